@@ -1,0 +1,204 @@
+"""bench.py — VQ-VAE train-step throughput on MI355X (BASELINE.json metric), one process per GPU.
+
+Workload (BASELINE config 2, "SMALL_VQ_VAE 3-level"): levels 3, latent 64, codebook 2048, down_depth
+[3,2,2], strides [2,2,2] (hops 8/32/128), residual width 32, depth 4, dilation factor 3; 65,536-frame
+44.1 kHz synthetic chunks, batch 32 per GPU, bf16 activations with fp32 weights / VQ state / Adam.
+A step = one full VQVAE.train_step (forward, spectral + MSE + commitment losses, backward, Keras Adam,
+codebook EMA with dead-code reset), replayed from a hipGraph. N > 1: data parallel (weak scaling), one
+RCCL all_reduce of [grads | EMA sums | reset rows | losses] per step.
+
+Prints ONE JSON line on rank 0. Also reports:
+  roofline     — the dominant kernel's algorithmic bytes / its average duration, measured with HIP events
+                 on its stream in an instrumented step after the timed region;
+  cpu_baseline — the oracle (torch-CPU fp32 restatement of the reference op sequence) timed on the host
+                 cores on a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "vae-based-music--deep-generative-models_amd")
+sys.path[:0] = [PKG, ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "audio-samples/sec/GPU VQ-VAE train step, 44.1kHz 65536-frame chunks @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CFG2 = dict(levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2], num_embeddings=2048,
+            residual_width=32, residual_depth=4, dilation_factor=3)
+DOMINANT = "gather_mfma_kernel<bf16, C=32, O=32, TM=256>"  # resblock forwards + stride-1 data-gradients
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=32, help="per-GPU batch")
+    p.add_argument("--seq", type=int, default=65536)
+    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-batch", type=int, default=4)
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+class KernelTimer:
+    """Wrap the libvqa conv entry points: HIP events around every launch that dispatches to the dominant
+    instantiation, plus its algorithmic bytes (input + output + residual + mask, activation dtype)."""
+
+    def __init__(self, V):
+        self.V = V
+        self.rec = []
+        self.orig = {}
+
+    @staticmethod
+    def _is_dominant(C, O, S, flags, dtype, V):
+        return dtype == V.BF16 and C == 32 and O == 32 and S == 1 and not (flags & (V.X_F32 | V.Y_F32))
+
+    def __enter__(self):
+        V = self.V
+        self.orig = {"fwd": V.conv1d_fwd, "bwd": V.conv1d_bwd_data}
+
+        def fwd(x, w, b, residual, y, B, T_in, T_out, C_in, C_out, K, stride, dil, pad, flags, dtype):
+            if self._is_dominant(C_in, C_out, stride, flags, dtype, V):
+                nbytes = 2 * (B * T_in * C_in + B * T_out * C_out * (2 if residual is not None else 1))
+                return self._timed(self.orig["fwd"], nbytes, x, w, b, residual, y, B, T_in, T_out, C_in, C_out, K,
+                                   stride, dil, pad, flags, dtype)
+            return self.orig["fwd"](x, w, b, residual, y, B, T_in, T_out, C_in, C_out, K, stride, dil, pad, flags,
+                                    dtype)
+
+        def bwd(dy, w, mask, residual, dx, B, T_in, T_out, C_in, C_out, K, stride, dil, pad, flags, dtype):
+            if self._is_dominant(C_out, C_in, stride, flags, dtype, V):
+                extra = (mask is not None) + (residual is not None)
+                nbytes = 2 * (B * T_out * C_out + B * T_in * C_in * (1 + extra))
+                return self._timed(self.orig["bwd"], nbytes, dy, w, mask, residual, dx, B, T_in, T_out, C_in, C_out,
+                                   K, stride, dil, pad, flags, dtype)
+            return self.orig["bwd"](dy, w, mask, residual, dx, B, T_in, T_out, C_in, C_out, K, stride, dil, pad,
+                                    flags, dtype)
+
+        V.conv1d_fwd, V.conv1d_bwd_data = fwd, bwd
+        return self
+
+    def _timed(self, fn, nbytes, *args):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(torch.cuda.current_stream())  # the stream libvqa launches on
+        fn(*args)
+        e.record(torch.cuda.current_stream())
+        self.rec.append((s, e, nbytes))
+
+    def __exit__(self, *a):
+        self.V.conv1d_fwd, self.V.conv1d_bwd_data = self.orig["fwd"], self.orig["bwd"]
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _ in self.rec]
+        nbytes = sum(b for _, _, b in self.rec)
+        return len(ms), float(np.sum(ms)), nbytes
+
+
+def cpu_baseline(batch, steps, seq):
+    from oracle import vqvae_ref as R
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = R.RefConfig(input_len=seq, **CFG2)
+    m = R.RefVQVAE(cfg, R.init_params(cfg, 1), R.init_vq_state(cfg, 2), dtype=torch.float32)
+    x = R.synthetic_batch(batch, seq, seed=999)
+    m.train_step(x)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.train_step(x)
+    dt = time.perf_counter() - t0
+    return {"value": batch * seq * steps / dt, "unit": "audio-samples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle torch-CPU fp32 train step (dense one-hot GEMMs, N x K distances, TF-style STFT) on "
+                      f"the cfg2 architecture, {batch} x {seq}-frame chunks, {steps} timed steps after 1 warm-up, "
+                      f"{threads} threads ({dt:.1f} s)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import vqa_lib as V
+    from data_utils import synthetic_batch
+    from vqvae import VQVAE
+
+    model = VQVAE((a.seq, 1), dtype=a.dtype, device=dev, **CFG2)
+    model.compile()
+    batches = [torch.from_numpy(synthetic_batch(a.batch, a.seq, seed=1234 + rank + 7919 * i)).to(dev)
+               for i in range(4)]
+    if not a.no_graph:
+        model.capture_train_step(batches[0], warmup=max(a.warmup, 1))
+    else:
+        for i in range(a.warmup):
+            model.train_step(batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        model.train_step(batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss = float(model.results()["loss"])
+
+    # roofline: one instrumented eager step (same launch set as a graph step)
+    with KernelTimer(V) as kt:
+        model._compute(batches[0], True)
+        model._update(True)
+    n_launch, ms_total, nbytes = kt.summary()
+    achieved = nbytes / (ms_total * 1e-3) / 1e9 if ms_total > 0 else 0.0
+    traffic = None
+    if os.path.exists(a.pmc_json):
+        try:
+            traffic = json.load(open(a.pmc_json)).get("per_launch_bytes")
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": DOMINANT,
+            "launches_per_step": n_launch, "avg_launch_us": round(ms_total * 1e3 / max(n_launch, 1), 2),
+            "algorithmic_bytes_per_launch": int(nbytes / max(n_launch, 1))}
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(a.cpu_batch, a.cpu_steps, a.seq)
+        value = a.batch * a.seq * a.steps * world / elapsed
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "audio-samples/s", "n_gpus": world,
+               "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+               "data": "synthetic 44.1 kHz sine+noise chunks (SURVEY.md §8d), random-init weights",
+               "config": {"workload": "SMALL_VQ_VAE 3-level VQ-VAE train step (BASELINE config 2)",
+                          "model": "VQVAE levels=3 latent=64 K=2048 down_depth=[3,2,2] width=32 depth=4 dil=3",
+                          "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",
+                          "graph": not a.no_graph, "final_loss": round(loss, 5)},
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * vqa.h — C-ABI of libvqa.so, the MI355X (gfx950) VQ-VAE audio training path.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (sunzeyucmu/VAE-based-Music--Deep-Generative-Models). The reference has no
+ * FFI: its "operator API" is the set of TensorFlow/Keras ops that its layers
+ * call. Each entry point below names the reference call site it replaces.
+ *
+ * Conventions (all entry points):
+ *  - Every pointer is a DEVICE pointer owned by the caller. The library never
+ *    allocates on the hot path; ops that need scratch take (workspace, bytes)
+ *    and expose a *_workspace() size query.
+ *  - Activations are channels-last (N, T, C) contiguous ("NTC"), exactly the
+ *    Keras layout. Their element type is `dtype` (VQA_F32 or VQA_BF16) unless a
+ *    VQA_X_F32 / VQA_Y_F32 flag forces fp32 on one side. Weights, biases,
+ *    gradients of weights, optimizer state and VQ state are always fp32.
+ *  - Keras kernel layouts: Conv1D (K, C_in, C_out); Conv1DTranspose
+ *    (K, C_out, C_in). Padding is TF "same" (see vqa_same_pad_left).
+ *  - Calls are asynchronous on `stream` (a hipStream_t; NULL = default stream)
+ *    and never synchronise. Every entry point returns VQA_OK (0) or a negative
+ *    VQA_E_* code; the message is in the thread-local vqa_get_last_error().
+ *    No C++ exception crosses the ABI. Entry points are reentrant.
+ */
+#ifndef VQA_H
+#define VQA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vqa_stream_t; /* hipStream_t */
+
+enum { VQA_OK = 0, VQA_E_INVALID_ARG = -1, VQA_E_UNSUPPORTED = -2, VQA_E_HIP = -3 };
+enum { VQA_F32 = 0, VQA_BF16 = 1 };
+
+/* conv flags */
+enum {
+  VQA_PRE_RELU = 1,     /* fwd / bwd_weight: use relu(x) (resnet.py:12,16 layers.ReLU before Conv1D) */
+  VQA_ADD_RESIDUAL = 2, /* out = residual + conv(...)   (resnet.py:29 layers.add)                     */
+  VQA_POST_MASK = 4,    /* out = (mask > 0) ? conv : 0  (ReLU backward, mask = pre-ReLU tensor)         */
+  VQA_X_F32 = 8,        /* the x / dx side tensor is fp32 regardless of dtype                          */
+  VQA_Y_F32 = 16        /* the y / dy side tensor is fp32 regardless of dtype                          */
+};
+
+/* ---- library -------------------------------------------------------------------------------- */
+const char* vqa_get_last_error(void);
+const char* vqa_version(void);
+/* TF SAME padding (Appendix A.2 of SURVEY.md): left pad of a conv with these parameters. Host-only. */
+int vqa_same_pad_left(int T_in, int K, int stride, int dilation);
+int vqa_same_out_len(int T_in, int stride);
+
+/* ---- Conv1D: replaces keras layers.Conv1D(filters, K, strides, dilation_rate, padding="same")
+ *      resnet.py:13, resnet.py:17, encdec.py:33 (down-sampling), encdec.py:38 (projection),
+ *      encdec.py:60 (decoder pre-conv), encdec.py:148 (decoder output conv)                      */
+int vqa_conv1d_fwd(const void* x, const float* w, const float* bias, const void* residual, void* y,
+                   int B, int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation,
+                   int pad_left, int flags, int dtype, vqa_stream_t stream);
+/* d(loss)/dx given dy (the GradientTape backward of the same layer, vqvae.py:143).
+ * flags: VQA_POST_MASK (mask has dx's shape), VQA_ADD_RESIDUAL (residual has dx's shape). */
+int vqa_conv1d_bwd_data(const void* dy, const float* w, const void* mask, const void* residual, void* dx,
+                        int B, int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation,
+                        int pad_left, int flags, int dtype, vqa_stream_t stream);
+/* dw (K, C_in, C_out) and db (C_out, nullable) — overwritten, not accumulated. flags: VQA_PRE_RELU. */
+int vqa_conv1d_bwd_weight(const void* x, const void* dy, float* dw, float* db,
+                          int B, int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation,
+                          int pad_left, int flags, int dtype, void* workspace, size_t ws_bytes,
+                          vqa_stream_t stream);
+size_t vqa_conv1d_bwd_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                                       int dilation, int pad_left, int flags, int dtype);
+
+/* ---- Conv1DTranspose: replaces keras layers.Conv1DTranspose(filters, 2*stride, strides=stride,
+ *      padding="same"), encdec.py:67-68. Supported: stride 2, K 4 (the reference's only use).
+ *      w is (K, C_out, C_in); T_out = stride*T_in.                                              */
+int vqa_conv1d_transpose_fwd(const void* x, const float* w, const float* bias, const void* residual, void* y,
+                             int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                             int pad_left, int flags, int dtype, vqa_stream_t stream);
+int vqa_conv1d_transpose_bwd_data(const void* dy, const float* w, const void* mask, const void* residual,
+                                  void* dx, int B, int T_in, int T_out, int C_in, int C_out, int K,
+                                  int stride, int pad_left, int flags, int dtype, vqa_stream_t stream);
+int vqa_conv1d_transpose_bwd_weight(const void* x, const void* dy, float* dw, float* db,
+                                    int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                                    int pad_left, int flags, int dtype, void* workspace, size_t ws_bytes,
+                                    vqa_stream_t stream);
+size_t vqa_conv1d_transpose_bwd_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K,
+                                                 int stride, int pad_left, int flags, int dtype);
+
+/* ---- Vector quantizer (VectorQuantizer.py) ---------------------------------------------------- */
+/* e_sqnorm[k] = sum_d E[d][k]^2  (VectorQuantizer.py:180). E is (D, K). */
+int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream);
+/* idx[n] = argmin_k (sum_d z[n][d]^2 + e_sqnorm[k]) - 2 * (z @ E)[n][k]; ties -> lowest k.
+ * Replaces get_code_indices, VectorQuantizer.py:170-186. min_dist nullable. z is (N, D) in dtype. */
+int vqa_vq_argmin(const void* z, const float* E, const float* e_sqnorm, int64_t* idx, float* min_dist,
+                  int64_t N, int D, int K, int dtype, vqa_stream_t stream);
+/* q = ET[idx] (one_hot @ E^T, :86-90); q_st = z + (q - z) (:114);
+ * commit_out[0] = beta * mean((q - z)^2) (:97-99);
+ * if m_sumT != NULL: m_sumT[k][d] += sum_{n: idx[n]=k} z[n][d], n_sum[k] += count (:123-124; the
+ * caller zeroes them first). ET is the (K, D) transpose of E kept by vqa_vq_ema_apply. */
+int vqa_vq_quantize(const void* z, const float* ET, const int64_t* idx, void* q_st, float* commit_out,
+                    float* m_sumT, float* n_sum, int64_t N, int D, int K, float beta, int dtype,
+                    void* workspace, size_t ws_bytes, vqa_stream_t stream);
+size_t vqa_vq_quantize_workspace(int64_t N, int D, int K, int dtype);
+/* Gradient of the quantizer: dz = dq_st + scale * (z - ET[idx])  (straight-through :114 plus the
+ * commitment term :97-99; scale = 2*beta/(N_global*D)). */
+int vqa_vq_backward(const void* dq, const void* z, const float* ET, const int64_t* idx, void* dz, float scale,
+                    int64_t N, int D, int dtype, vqa_stream_t stream);
+/* Dead-code reset candidates (VectorQuantizer.py:137 shuffle(_tile(flat))[:K], _tile :191-199) with an
+ * injected permutation: RT[k][:] = z_global[perm(k) mod N_global] if that row lives on this rank
+ * (global rows [row_offset, row_offset + N_local)), else 0. perm = vqa_reset_perm_index(seed,
+ * *counter, level, M, k) with M = N_global (or N_global*ceil(K/N_global) when N_global < K). */
+int vqa_vq_reset_rows(const void* z, float* RT, int64_t N_local, int64_t row_offset, int64_t N_global,
+                      int D, int K, uint64_t seed, const int64_t* counter, int level, int dtype,
+                      vqa_stream_t stream);
+/* EMA codebook update (VectorQuantizer.py:126-145) from (all-reduced) m_sumT/n_sum/RT:
+ * N_t = g*N_t + omg*n_sum; m_t = g*m_t + omg*m_sum; usage = N_t >= thresh;
+ * E = usage ? m_t / clip(N_t, 1e-8, 1e8) : R; ET = E^T. Increments *counter.
+ * metrics[0..2] = batch usage, running usage, entropy (VectorQuantizer.py:149-159). */
+int vqa_vq_ema_apply(float* E, float* ET, float* m_t, float* N_t, const float* m_sumT, const float* n_sum,
+                     const float* RT, float gamma, float one_minus_gamma, float thresh, float* metrics,
+                     int64_t* counter, int D, int K, vqa_stream_t stream);
+/* The reset permutation (host-callable; the device uses the same code): a keyed 4-round Feistel
+ * bijection on [0, M) with cycle walking. Returns the k-th sampled row of the tiled batch. */
+int64_t vqa_reset_perm_index(uint64_t seed, int64_t counter, int level, int64_t M, int64_t k);
+
+/* ---- losses / optimizer ------------------------------------------------------------------------ */
+/* loss_out[0] = mean((r - x)^2) (vqvae.py:91,125); dr = 2*(r - x)/n + extra (extra nullable). fp32. */
+int vqa_mse_loss(const float* x, const float* r, const float* extra_grad, float* dr, float* loss_out,
+                 int64_t n, void* workspace, size_t ws_bytes, vqa_stream_t stream);
+size_t vqa_mse_loss_workspace(int64_t n);
+/* Keras 2.7 Adam (vqvae.py:144, compile at :362; TF ApplyAdam): t = *step + 1,
+ * alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g*s - m)(1-b1); v += ((g*s)^2 - v)(1-b2);
+ * w -= alpha*m/(sqrt(v)+eps), with s = grad_scale. Does not touch *step. */
+int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, const int64_t* step, float lr,
+                   float beta1, float beta2, float eps, float grad_scale, vqa_stream_t stream);
+/* *counter += delta on the stream (graph-capturable step counters). */
+int vqa_counter_add(int64_t* counter, int64_t delta, vqa_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VQA_H */

@@ -1,0 +1,157 @@
+"""Vector-quantizer kernel parity (VectorQuantizer.py:75-199) vs the CPU oracle.
+
+Indices are compared bit-exactly on every row whose fp64 top-2 distance margin exceeds
+1e-5 * |d_min|; near-tie rows are counted and must be rare. Everything else fp32 within
+1e-6..1e-5 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+import vqa_lib as V
+from oracle import reset_perm
+from VectorQuantizer import VectorQuantizer
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_dist(z, E):
+    z = z.double()
+    E = E.double()
+    return (z * z).sum(1, keepdim=True) + (E * E).sum(0) - 2 * z @ E
+
+
+def _margin_mask(d):
+    top2 = torch.topk(d, 2, dim=1, largest=False).values
+    margin = top2[:, 1] - top2[:, 0]
+    return margin > 1e-5 * top2[:, 0].abs().clamp(min=1e-12)
+
+
+@pytest.mark.parametrize("D,K,N", [(64, 2048, 20000), (64, 256, 2048), (8, 1024, 512), (4, 16, 1000),
+                                   (16, 100, 333), (6, 50, 77)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_argmin_exact(cuda, D, K, N, dt):
+    g = torch.Generator().manual_seed(D * 7 + K)
+    z = torch.randn(N, D, generator=g).to(dt)
+    E = (torch.rand(D, K, generator=g) - 0.5) * 0.1 + 0.05 * torch.randn(D, K, generator=g)
+    zd, Ed = z.to(cuda), E.to(cuda)
+    esq = torch.empty(K, device=cuda)
+    V.vq_sqnorm(Ed, esq)
+    idx = torch.empty(N, dtype=torch.int64, device=cuda)
+    mind = torch.empty(N, device=cuda)
+    V.vq_argmin(zd, Ed, esq, idx, mind)
+    d = _ref_dist(z.float(), E)
+    ref = d.argmin(1)
+    ok = _margin_mask(d)
+    got = idx.cpu()
+    assert ok.float().mean() > 0.99
+    assert torch.equal(got[ok], ref[ok]), f"{int((got[ok] != ref[ok]).sum())} mismatches on clear rows"
+    # min distance equals the fp32 distance of the chosen code
+    assert torch.allclose(mind.cpu().double(), d.gather(1, got[:, None]).squeeze(1), rtol=1e-5, atol=1e-5)
+
+
+def test_argmin_ties_lowest_index(cuda):
+    D, K = 64, 512
+    E = torch.zeros(D, K)
+    E[:, 7] = 1.0
+    E[:, 300] = 1.0     # duplicate code
+    E[:, 301] = 1.0
+    z = torch.ones(40, D)
+    z[20:] = 0.0        # equidistant to every zero column -> lowest zero column (0)
+    Ed, zd = E.cuda(), z.cuda()
+    esq = torch.empty(K, device=cuda)
+    V.vq_sqnorm(Ed, esq)
+    idx = torch.empty(40, dtype=torch.int64, device=cuda)
+    V.vq_argmin(zd, Ed, esq, idx)
+    got = idx.cpu()
+    assert (got[:20] == 7).all() and (got[20:] == 0).all()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_quantize_commit_stats_backward(cuda, dt):
+    N, D, K, beta = 5000, 64, 256, 0.25
+    g = torch.Generator().manual_seed(5)
+    z = torch.randn(N, D, generator=g).to(dt)
+    E = torch.randn(D, K, generator=g) * 0.3
+    idx = torch.randint(0, K, (N,), generator=g)
+    zd, ETd, idxd = z.cuda(), E.t().contiguous().cuda(), idx.cuda()
+    q = torch.empty_like(zd)
+    commit = torch.zeros(1, device=cuda)
+    m_sumT = torch.zeros(K, D, device=cuda)
+    n_sum = torch.zeros(K, device=cuda)
+    V.vq_quantize(zd, ETd, idxd, q, commit, m_sumT, n_sum, beta)
+    zf = z.double()
+    qref = E.t()[idx].double()
+    # straight-through value z + (q - z) computed in fp32 then stored (VectorQuantizer.py:114)
+    st = (z.float() + (E.t()[idx] - z.float())).to(dt)
+    assert torch.equal(q.cpu(), st)
+    assert abs(float(commit) - beta * float(((qref - zf) ** 2).mean())) < 1e-5 * float(commit)
+    onehot = torch.nn.functional.one_hot(idx, K).double()
+    assert torch.allclose(m_sumT.cpu().double(), (zf.T @ onehot).T, rtol=1e-5, atol=1e-4)
+    assert torch.equal(n_sum.cpu(), onehot.sum(0).float())
+    dq = torch.randn(N, D, generator=g).to(dt)
+    dz = torch.empty_like(zd)
+    scale = 2 * beta / (N * D)
+    V.vq_backward(dq.cuda(), zd, ETd, idxd, dz, scale)
+    ref = (dq.float() + scale * (z.float() - E.t()[idx])).to(dt)
+    assert torch.allclose(dz.cpu().float(), ref.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,K", [(20000, 2048), (100, 256), (1000, 1000)])
+def test_reset_rows_match_numpy_permutation(cuda, N, K):
+    D = 8
+    z = torch.randn(N, D).cuda()
+    RT = torch.empty(K, D, device=cuda)
+    counter = torch.tensor([5], dtype=torch.int64, device=cuda)
+    V.vq_reset_rows(z, RT, 0, N, 3, counter, 1)
+    rows = reset_perm.reset_rows(3, 5, 1, N, K)
+    assert torch.equal(RT.cpu(), z.cpu()[torch.from_numpy(rows)])
+    # sharded: two "ranks" each own half the rows; the sum of their partial RT is the global one
+    half = N // 2
+    RT0, RT1 = torch.empty_like(RT), torch.empty_like(RT)
+    V.vq_reset_rows(z[:half].contiguous(), RT0, 0, N, 3, counter, 1)
+    V.vq_reset_rows(z[half:].contiguous(), RT1, half, N, 3, counter, 1)
+    assert torch.equal((RT0 + RT1).cpu(), RT.cpu())
+
+
+def test_ema_apply_matches_reference_formula(cuda):
+    D, K = 64, 512
+    g = torch.Generator().manual_seed(9)
+    E = (torch.rand(D, K, generator=g) - 0.5) * 0.1
+    m_t = E.clone()
+    N_t = torch.ones(K)
+    n_sum = torch.zeros(K)
+    n_sum[:100] = torch.randint(1, 50, (100,), generator=g).float()
+    m_sumT = torch.randn(K, D, generator=g) * n_sum[:, None]
+    RT = torch.randn(K, D, generator=g)
+    Ed, ETd, mtd, Ntd = E.cuda(), E.t().contiguous().cuda(), m_t.cuda(), N_t.cuda()
+    met = torch.zeros(3, device=cuda)
+    ctr = torch.zeros(1, dtype=torch.int64, device=cuda)
+    gam, omg = float(np.float32(0.99)), float(np.float32(1 - 0.99))
+    V.vq_ema_apply(Ed, ETd, mtd, Ntd, m_sumT.cuda(), n_sum.cuda(), RT.cuda(), gam, omg, 1.0, met, ctr)
+    # fp32 restatement of VectorQuantizer.py:128-145 (numpy float32, no fused multiply-add)
+    f = np.float32
+    Nn = f(gam) * N_t.numpy() + f(omg) * n_sum.numpy()
+    mn = f(gam) * m_t.numpy() + f(omg) * m_sumT.numpy().T
+    use = (Nn >= 1.0).astype(np.float32)[None, :]
+    En = use * (mn / np.clip(Nn, f(1e-8), f(1e8))[None, :]) + (1 - use) * RT.numpy().T
+    assert np.array_equal(Ntd.cpu().numpy(), Nn)
+    assert np.array_equal(mtd.cpu().numpy(), mn)
+    assert np.allclose(Ed.cpu().numpy(), En, rtol=2e-7, atol=0)
+    assert torch.equal(ETd.cpu(), Ed.cpu().t())
+    assert int(ctr) == 1
+    p = n_sum / n_sum.sum()
+    assert float(met[0]) == float((n_sum >= 1).sum())
+    assert float(met[1]) == float((torch.from_numpy(Nn) >= 1).sum())
+    assert abs(float(met[2]) + float((p * torch.log(p + 1e-8)).sum())) < 1e-4
+
+
+def test_vector_quantizer_layer_call(cuda):
+    """VectorQuantizer.py:204-221 smoke: K=6, D=2 — the generic (D not MFMA-tiled) path."""
+    torch.manual_seed(0)
+    vq = VectorQuantizer(num_embeddings=6, embedding_dim=2, device=cuda)
+    x = torch.randn(32, 100, 2, device=cuda)
+    q, idx = vq(x)
+    assert q.shape == x.shape and idx.shape == (3200,)
+    assert torch.isfinite(vq.embeddings).all()
+    assert float(vq.N_t.sum()) > 0

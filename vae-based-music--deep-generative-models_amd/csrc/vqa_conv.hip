@@ -1,0 +1,755 @@
+// vqa_conv.hip — 1-D convolution kernels for the dilated-conv encoder/decoder (gfx950).
+//
+// Replaces the TF ops behind keras Conv1D / Conv1DTranspose on the reference's hot path:
+//   resnet.py:13,17 (dilated residual convs), encdec.py:33 (strided down conv), :38 (projection),
+//   :60 (decoder pre-conv), :67-68 (Conv1DTranspose up conv), :148 (decoder output conv).
+//
+// Every forward and data-gradient is ONE "gather" convolution
+//     y[n, t, o] = sum_{k, c} act(x[n, t*S + k*D - P, c]) * Weff[k][c][o]      (+bias, mask, residual)
+// with three ways of reading the fp32 Keras weight ("wmode"):
+//   DIRECT : Weff = W[k][c][o]                       conv fwd; conv-transpose data-grad (stride 2)
+//   FLIP_T : Weff = W[Kb-1-k][o][c]                  stride-1 conv data-grad
+//   PAIR   : out pair j holds full rows 2j, 2j+1:    conv-transpose fwd; stride-2 conv data-grad
+//            Weff[a+1][c][p*Ob+ob] = W[p + Pb - 2a][ob][c]  (a in {-1,0,1}, zero when out of range)
+// so the MFMA kernel below covers all of them; the PAIR layout (n, j, p, ob) is exactly the NTC
+// layout of the full-resolution tensor. Weight gradients are split-row MFMA reductions with
+// per-workgroup fp32 partials and a deterministic second pass.
+#include "vqa_common.h"
+#include <algorithm>
+
+namespace vqa {
+
+enum { W_DIRECT = 0, W_FLIP_T = 1, W_PAIR = 2 };
+
+struct GatherArgs {
+  const void* x;
+  const float* w;
+  const float* bias;
+  const void* resid;
+  const void* mask;
+  void* y;
+  int B, T_in, T_out;  // x rows per item, gather-output rows per item
+  int C, O;            // gather input / output channels
+  int K, S, D, P;      // gather taps, stride, dilation, left pad
+  int wmode, Kb, Pb;   // weight mapping; base taps; base pad (PAIR)
+  int T_full;          // PAIR: full-resolution rows per item (store guard)
+  int flags;
+};
+
+__device__ __forceinline__ float weff(const GatherArgs& a, int k, int c, int o) {
+  if (a.wmode == W_DIRECT) return a.w[((size_t)k * a.C + c) * a.O + o];
+  if (a.wmode == W_FLIP_T) return a.w[((size_t)(a.Kb - 1 - k) * a.O + o) * a.C + c];
+  const int Ob = a.O >> 1;
+  const int p = o >= Ob ? 1 : 0;
+  const int ob = o - p * Ob;
+  const int kb = p + a.Pb - 2 * (k - 1);
+  return (kb >= 0 && kb < a.Kb) ? a.w[((size_t)kb * Ob + ob) * a.C + c] : 0.f;
+}
+
+// output element index (n, t, o) -> linear offset in y / resid / mask, or -1 if outside (PAIR tail)
+__device__ __forceinline__ long long out_index(const GatherArgs& a, int n, int t, int o) {
+  if (a.wmode == W_PAIR) {
+    const int Ob = a.O >> 1;
+    const int p = o >= Ob ? 1 : 0;
+    const int u = 2 * t + p;
+    if (u >= a.T_full) return -1;
+    return ((long long)n * a.T_full + u) * Ob + (o - p * Ob);
+  }
+  return ((long long)n * a.T_out + t) * a.O + o;
+}
+
+__device__ __forceinline__ int bias_index(const GatherArgs& a, int o) {
+  return a.wmode == W_PAIR ? (o >= (a.O >> 1) ? o - (a.O >> 1) : o) : o;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Generic VALU gather conv: any C/O/K/S/D, mixed fp32/bf16 ends. Used for the 1-channel layers at
+// the waveform ends (first encoder conv C=1, decoder output conv O=1 and its data-gradient).
+template <class TX, class TY>
+__global__ __launch_bounds__(256) void gather_direct_kernel(GatherArgs a) {
+  const TX* X = (const TX*)a.x;
+  const long long total = (long long)a.B * a.T_out * a.O;
+  const bool relu = a.flags & VQA_PRE_RELU;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(e % a.O);
+    const long long r = e / a.O;
+    const int t = (int)(r % a.T_out);
+    const int n = (int)(r / a.T_out);
+    float acc = 0.f;
+    for (int k = 0; k < a.K; ++k) {
+      const int ti = t * a.S + k * a.D - a.P;
+      if (ti < 0 || ti >= a.T_in) continue;
+      const TX* xr = X + ((long long)n * a.T_in + ti) * a.C;
+      for (int c = 0; c < a.C; ++c) {
+        float xv = ld(xr + c);
+        if (relu) xv = fmaxf(xv, 0.f);
+        acc += xv * weff(a, k, c, o);
+      }
+    }
+    const long long oi = out_index(a, n, t, o);
+    if (oi < 0) continue;
+    float v = acc;
+    if (a.bias) v = v + a.bias[bias_index(a, o)];
+    if (a.flags & VQA_POST_MASK) v = ld((const TY*)a.mask + oi) > 0.f ? v : 0.f;
+    if (a.flags & VQA_ADD_RESIDUAL) v = ld((const TY*)a.resid + oi) + v;
+    st((TY*)a.y + oi, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// MFMA fragment traits. bf16: v_mfma_f32_16x16x32_bf16 (8 consecutive channels per lane, one
+// 16-byte LDS read). fp32: v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain; used for parity runs).
+template <class T> struct Mfma;
+template <> struct Mfma<bf16> {
+  static constexpr int KS = 32;
+  typedef bf16x8 frag;
+  static __device__ __forceinline__ int koff(int lane) { return 8 * (lane >> 4); }
+  static __device__ __forceinline__ frag load(const bf16* p) { return *(const bf16x8*)p; }
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  // 8 elements with a row stride (strided LDS gather; used by the weight-gradient kernel)
+  static __device__ __forceinline__ frag gather(const bf16* p, int stride) {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = p[j * stride];
+    return f;
+  }
+};
+template <> struct Mfma<float> {
+  static constexpr int KS = 4;
+  typedef float frag;
+  static __device__ __forceinline__ int koff(int lane) { return lane >> 4; }
+  static __device__ __forceinline__ frag load(const float* p) { return *p; }
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag gather(const float* p, int) { return *p; }
+};
+
+template <class T> __device__ __forceinline__ void relu_bits(uint4& v);
+template <> __device__ __forceinline__ void relu_bits<bf16>(uint4& v) {
+  uint32_t* w = (uint32_t*)&v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] &= ~(((w[i] >> 15) & 0x00010001u) * 0xFFFFu);
+}
+template <> __device__ __forceinline__ void relu_bits<float>(uint4& v) {
+  uint32_t* w = (uint32_t*)&v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] &= ~(uint32_t)((int32_t)w[i] >> 31);
+}
+
+template <class T> constexpr int lds_pad() { return 16 / (int)sizeof(T); }
+
+// Stage rows [r0, r0+rows) of one item (Xi = that item's row 0, channels C) into LDS with padded row
+// stride XS, zero-filling rows outside [lo, hi), optional ReLU. 16-byte vector loads.
+template <class T, int C>
+__device__ __forceinline__ void stage_rows(T* xl, int XS, const T* Xi, int lo, int hi, int r0, int rows,
+                                           bool relu) {
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int CPR = C / VEC;
+  for (int e = threadIdx.x; e < rows * CPR; e += blockDim.x) {
+    const int rr = e / CPR, q = e - rr * CPR;
+    const int ti = r0 + rr;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (ti >= lo && ti < hi) v = *((const uint4*)(Xi + (long long)ti * C) + q);
+    if (relu) relu_bits<T>(v);
+    *(uint4*)(xl + rr * XS + q * VEC) = v;
+  }
+}
+
+// MFMA gather conv. One workgroup = 4 waves = TM output rows of one item x all O channels.
+// D[o][t] = sum_{k,c} Weff^T[o][(k,c)] * X[(k,c)][t]: the A operand is the weight (rows = output
+// channels), the B operand a 16-byte channel run of one input row, so each lane of the accumulator
+// holds 4 consecutive output channels of one time step (8- or 16-byte stores).
+template <class T, int C, int O, int TM>
+__global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a) {
+  typedef Mfma<T> M;
+  constexpr int NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
+  constexpr int XS = C + lds_pad<T>();
+  constexpr int WS = C + lds_pad<T>();
+  static_assert(RW % 16 == 0 && O % 16 == 0 && C % M::KS == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* wl = (T*)smem;
+  T* xl = wl + (size_t)a.K * O * WS;
+
+  const int n = blockIdx.y;
+  const int t0 = blockIdx.x * TM;
+  const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
+
+  for (int e = threadIdx.x; e < a.K * O * C; e += blockDim.x) {
+    const int c = e % C, o = (e / C) % O, k = e / (C * O);
+    wl[(k * O + o) * WS + c] = (T)weff(a, k, c, o);
+  }
+  stage_rows<T, C>(xl, XS, (const T*)a.x + (long long)n * a.T_in * C, 0, a.T_in, t0 * a.S - a.P, rows_in,
+                   a.flags & VQA_PRE_RELU);
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ko = M::koff(lane);
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k = 0; k < a.K; ++k) {
+    const T* wk = wl + (size_t)k * O * WS + (lane & 15) * WS + ko;
+    const T* xk = xl + (size_t)(k * a.D) * XS + ko;
+#pragma unroll
+    for (int cc = 0; cc < C; cc += M::KS) {
+      typename M::frag af[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) af[mt] = M::load(wk + mt * 16 * WS + cc);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int tl = wave * RW + nt * 16 + (lane & 15);
+        const typename M::frag bf = M::load(xk + (size_t)(tl * a.S) * XS + cc);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = M::mma(af[mt], bf, acc[mt][nt]);
+      }
+    }
+  }
+
+  const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int t = t0 + wave * RW + nt * 16 + (lane & 15);
+    if (t >= a.T_out) continue;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int o = mt * 16 + 4 * (lane >> 4);
+      const long long oi = out_index(a, n, t, o);
+      if (oi < 0) continue;
+      f32x4 v = acc[mt][nt];
+      if (a.bias) {
+        const float* bp = a.bias + bias_index(a, o);
+        v = f32x4{v[0] + bp[0], v[1] + bp[1], v[2] + bp[2], v[3] + bp[3]};
+      }
+      if (do_mask) {
+        const f32x4 m = ld4((const T*)a.mask + oi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
+      }
+      if (do_res) {
+        const f32x4 r = ld4((const T*)a.resid + oi);
+        v = f32x4{r[0] + v[0], r[1] + v[1], r[2] + v[2], r[3] + v[3]};
+      }
+      st4((T*)a.y + oi, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient: dW[k][c][o] = sum_{n,t} act(x[n, t*S + k*D - P, c]) * g[n, t, o],
+// db[o] = sum_{n,t} g[n, t, o]. Grid = (chunks per item, items); each workgroup reduces CH output
+// rows in TT-row sub-tiles staged in LDS and writes fp32 partials [wg][K*C*O + O]; a second
+// kernel sums the partials in a fixed order (deterministic).
+struct WgradArgs {
+  const void* x;
+  const void* g;
+  float* ws;
+  int B, T_in, T_out, C, O, K, S, D, P;
+  int CH, nchunk;
+  int flags;
+};
+
+template <class T, int C, int O, int TT>
+__global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
+  typedef Mfma<T> M;
+  constexpr int XS = C + lds_pad<T>();
+  constexpr int GS = O + lds_pad<T>();
+  constexpr int CT = C / 16, OT = O / 16;
+  constexpr int MAXTW = CT * OT;  // max tiles per wave (K <= 4 taps over 4 waves)
+  constexpr int KT = (int)sizeof(T) == 2 ? 32 : 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* gl = (T*)smem;
+  T* xl = gl + TT * GS;
+  __shared__ float red[256];
+
+  const int n = blockIdx.y, ch = blockIdx.x;
+  const int tbeg = ch * a.CH, tend = min(a.T_out, tbeg + a.CH);
+  const int rows_in = (TT - 1) * a.S + (a.K - 1) * a.D + 1;
+  const int ntile = a.K * CT * OT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ko = (int)sizeof(T) == 2 ? 8 * (lane >> 4) : (lane >> 4);
+
+  f32x4 acc[MAXTW];
+#pragma unroll
+  for (int i = 0; i < MAXTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;
+  const int dbo = threadIdx.x % O, dbr = threadIdx.x / O;
+  constexpr int DBSTEP = 256 / O;
+
+  for (int t0 = tbeg; t0 < tend; t0 += TT) {
+    const int nrows = min(TT, tend - t0);
+    stage_rows<T, O>(gl, GS, (const T*)a.g + (long long)n * a.T_out * O, t0, t0 + nrows, t0, TT, false);
+    stage_rows<T, C>(xl, XS, (const T*)a.x + (long long)n * a.T_in * C, 0, a.T_in, t0 * a.S - a.P, rows_in,
+                     a.flags & VQA_PRE_RELU);
+    __syncthreads();
+    for (int r = dbr; r < nrows; r += DBSTEP) dbacc += (float)gl[r * GS + dbo];
+#pragma unroll
+    for (int ti = 0; ti < MAXTW; ++ti) {
+      const int tile = wave + 4 * ti;
+      if (tile < ntile) {
+        const int ot = tile % OT, rest = tile / OT, ct = rest % CT, k = rest / CT;
+        const T* xp = xl + (size_t)(k * a.D + ko * a.S) * XS + ct * 16 + (lane & 15);
+        const T* gp = gl + (size_t)ko * GS + ot * 16 + (lane & 15);
+        f32x4 c = acc[ti];
+        for (int kk = 0; kk < TT; kk += KT) {
+          const typename M::frag af = M::gather(xp + (size_t)(kk * a.S) * XS, a.S * XS);
+          const typename M::frag bf = M::gather(gp + (size_t)kk * GS, GS);
+          c = M::mma(af, bf, c);
+        }
+        acc[ti] = c;
+      }
+    }
+    __syncthreads();
+  }
+
+  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(a.K * C * O + O);
+#pragma unroll
+  for (int ti = 0; ti < MAXTW; ++ti) {
+    const int tile = wave + 4 * ti;
+    if (tile < ntile) {
+      const int ot = tile % OT, rest = tile / OT, ct = rest % CT, k = rest / CT;
+      const int o = ot * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = ct * 16 + 4 * (lane >> 4) + r;
+        out[((size_t)k * C + c) * O + o] = acc[ti][r];
+      }
+    }
+  }
+  red[threadIdx.x] = dbacc;
+  __syncthreads();
+  if (threadIdx.x < O) {
+    float s = 0.f;
+    for (int r = 0; r < DBSTEP; ++r) s += red[r * O + threadIdx.x];
+    out[a.K * C * O + threadIdx.x] = s;
+  }
+}
+
+// Generic VALU weight gradient (small K*C*O: the 1-channel layers). Same partial layout.
+template <class TX, class TG, int TT>
+__global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* gl = (float*)smem;           // [TT][O]
+  float* xl = gl + TT * a.O;          // [rows_in][C]
+  constexpr int EPT = 16;
+  const int n = blockIdx.y, ch = blockIdx.x;
+  const int tbeg = ch * a.CH, tend = min(a.T_out, tbeg + a.CH);
+  const int rows_in = (TT - 1) * a.S + (a.K - 1) * a.D + 1;
+  const int E = a.K * a.C * a.O;
+  const bool relu = a.flags & VQA_PRE_RELU;
+  float acc[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) acc[i] = 0.f;
+  float dbacc = 0.f;
+  for (int t0 = tbeg; t0 < tend; t0 += TT) {
+    const int nrows = min(TT, tend - t0);
+    for (int e = threadIdx.x; e < TT * a.O; e += blockDim.x) {
+      const int r = e / a.O, o = e - r * a.O;
+      gl[e] = r < nrows ? ld((const TG*)a.g + ((long long)n * a.T_out + t0 + r) * a.O + o) : 0.f;
+    }
+    for (int e = threadIdx.x; e < rows_in * a.C; e += blockDim.x) {
+      const int r = e / a.C, c = e - r * a.C;
+      const int ti = t0 * a.S - a.P + r;
+      float v = (ti >= 0 && ti < a.T_in) ? ld((const TX*)a.x + ((long long)n * a.T_in + ti) * a.C + c) : 0.f;
+      xl[e] = relu ? fmaxf(v, 0.f) : v;
+    }
+    __syncthreads();
+    if (threadIdx.x < a.O)
+      for (int r = 0; r < nrows; ++r) dbacc += gl[r * a.O + threadIdx.x];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < E) {
+        const int o = e % a.O, c = (e / a.O) % a.C, k = e / (a.O * a.C);
+        float s = acc[i];
+        for (int r = 0; r < nrows; ++r) s += xl[(r * a.S + k * a.D) * a.C + c] * gl[r * a.O + o];
+        acc[i] = s;
+      }
+    }
+    __syncthreads();
+  }
+  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(E + a.O);
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = threadIdx.x + i * 256;
+    if (e < E) out[e] = acc[i];
+  }
+  if (threadIdx.x < a.O) out[E + threadIdx.x] = dbacc;
+}
+
+// out1[e] = sum_p ws[p*E + e] for e < E1; out2[e - E1] likewise for e >= E1 (fixed order).
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, int nparts, int E, int E1,
+                                                             float* out1, float* out2) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += ws[(size_t)p * E + e];
+  if (e < E1) {
+    if (out1) out1[e] = s;
+  } else if (out2) {
+    out2[e - E1] = s;
+  }
+}
+
+// column sums of a (rows, O) tensor: partial per workgroup -> ws[wg][O]
+template <class T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* y, long long rows, int O, int rows_per_wg,
+                                                            float* ws) {
+  __shared__ float red[256];
+  const long long r0 = (long long)blockIdx.x * rows_per_wg;
+  const long long r1 = min(rows, r0 + rows_per_wg);
+  const int o = threadIdx.x % O, rs = threadIdx.x / O, step = 256 / O;
+  float s = 0.f;
+  for (long long r = r0 + rs; r < r1; r += step) s += ld(y + r * O + o);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < O) {
+    float t = 0.f;
+    for (int i = 0; i < step; ++i) t += red[i * O + threadIdx.x];
+    ws[(size_t)blockIdx.x * O + threadIdx.x] = t;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// Raise a kernel's dynamic-LDS limit only when a launch needs more than the 64 KiB default; the value is
+// the exact need (static LDS counts against the 160 KiB too). Cached per kernel, so it runs during the
+// eager warm-up, never inside a hipGraph capture.
+static int ensure_dyn_lds(const void* fn, size_t bytes, size_t* cached, const char* name) {
+  if (bytes <= 65536 || bytes <= *cached) return VQA_OK;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    vqa::set_error("%s: cannot reserve %zu B of LDS: %s", name, bytes, hipGetErrorString(e));
+    return VQA_E_UNSUPPORTED;
+  }
+  *cached = bytes;
+  return VQA_OK;
+}
+static int gather_tm(int O, int S) {
+  if (O == 32) return S == 1 ? 256 : 128;
+  if (O == 64) return 128;
+  return 64;
+}
+
+template <class T, int C, int O, int TM>
+static int launch_gather_mfma_t(const GatherArgs& a, hipStream_t s) {
+  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>();
+  const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
+  const size_t lds = ((size_t)a.K * O * WS + (size_t)rows_in * XS) * sizeof(T);
+  VQA_REQUIRE(lds <= 160 * 1024, VQA_E_UNSUPPORTED, "gather conv: LDS tile too large (%zu B)", lds);
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds((const void*)gather_mfma_kernel<T, C, O, TM>, lds, &lds_set, "gather_mfma_kernel");
+  if (rc != VQA_OK) return rc;
+  dim3 grid((a.T_out + TM - 1) / TM, a.B);
+  hipLaunchKernelGGL((gather_mfma_kernel<T, C, O, TM>), grid, dim3(256), lds, s, a);
+  VQA_LAUNCHED("gather_mfma_kernel");
+  return VQA_OK;
+}
+
+template <class T, int C, int O>
+static int launch_gather_mfma_o(const GatherArgs& a, hipStream_t s) {
+  const int tm = gather_tm(O, a.S);
+  if (O == 32) {
+    if (tm == 256) return launch_gather_mfma_t<T, C, O, 256>(a, s);
+    return launch_gather_mfma_t<T, C, O, 128>(a, s);
+  }
+  if (O == 64) return launch_gather_mfma_t<T, C, O, 128>(a, s);
+  return launch_gather_mfma_t<T, C, O, 64>(a, s);
+}
+
+template <class T>
+static int launch_gather_mfma(const GatherArgs& a, hipStream_t s) {
+  if (a.C == 32) {
+    if (a.O == 32) return launch_gather_mfma_o<T, 32, 32>(a, s);
+    if (a.O == 64) return launch_gather_mfma_o<T, 32, 64>(a, s);
+    if (a.O == 128) return launch_gather_mfma_o<T, 32, 128>(a, s);
+  } else if (a.C == 64) {
+    if (a.O == 32) return launch_gather_mfma_o<T, 64, 32>(a, s);
+    if (a.O == 64) return launch_gather_mfma_o<T, 64, 64>(a, s);
+    if (a.O == 128) return launch_gather_mfma_o<T, 64, 128>(a, s);
+  }
+  vqa::set_error("gather conv: no MFMA tile for C=%d O=%d", a.C, a.O);
+  return VQA_E_UNSUPPORTED;
+}
+
+static bool mfma_ok(const GatherArgs& a) {
+  if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return false;
+  if (!((a.C == 32 || a.C == 64) && (a.O == 32 || a.O == 64 || a.O == 128))) return false;
+  const int tm = gather_tm(a.O, a.S);
+  const int rows_in = (tm - 1) * a.S + (a.K - 1) * a.D + 1;
+  return (size_t)rows_in * (a.C + 8) * 4 + (size_t)a.K * a.O * (a.C + 8) * 4 <= 150 * 1024;
+}
+
+template <class TX, class TY>
+static int launch_gather_direct(const GatherArgs& a, hipStream_t s) {
+  const long long total = (long long)a.B * a.T_out * a.O;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((gather_direct_kernel<TX, TY>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  VQA_LAUNCHED("gather_direct_kernel");
+  return VQA_OK;
+}
+
+int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
+  VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
+  VQA_ARG(a.x && a.w && a.y, "null tensor pointer");
+  VQA_ARG(a.B > 0 && a.T_in > 0 && a.T_out > 0 && a.C > 0 && a.O > 0 && a.K > 0 && a.S > 0 && a.D > 0,
+          "non-positive shape");
+  VQA_ARG(!(a.flags & VQA_POST_MASK) || a.mask, "VQA_POST_MASK without mask");
+  VQA_ARG(!(a.flags & VQA_ADD_RESIDUAL) || a.resid, "VQA_ADD_RESIDUAL without residual");
+  if (mfma_ok(a)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
+  const bool xf = dtype == VQA_F32 || (a.flags & VQA_X_F32);
+  const bool yf = dtype == VQA_F32 || (a.flags & VQA_Y_F32);
+  if (xf && yf) return launch_gather_direct<float, float>(a, s);
+  if (xf) return launch_gather_direct<float, bf16>(a, s);
+  if (yf) return launch_gather_direct<bf16, float>(a, s);
+  return launch_gather_direct<bf16, bf16>(a, s);
+}
+
+// ---- weight gradient planning ----
+struct WgradPlan {
+  bool mfma;
+  int TT, CH, nchunk, nwg, E;
+  size_t lds, ws_bytes;
+};
+
+static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O, int K, int S, int D, int flags) {
+  WgradPlan p{};
+  const bool anyf32 = (flags & (VQA_X_F32 | VQA_Y_F32)) != 0;
+  p.mfma = !anyf32 && (C == 32 || C == 64) && (O == 32 || O == 64) && K <= 4;
+  const size_t esz = dtype == VQA_BF16 ? 2 : 4;
+  if (p.mfma) {
+    p.TT = dtype == VQA_BF16 ? 256 : 128;
+    const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
+    p.lds = ((size_t)p.TT * (O + 16 / esz) + (size_t)rows_in * (C + 16 / esz)) * esz;
+    if (p.lds > 150 * 1024) {
+      p.TT = 64;
+      const int r2 = (p.TT - 1) * S + (K - 1) * D + 1;
+      p.lds = ((size_t)p.TT * (O + 16 / esz) + (size_t)r2 * (C + 16 / esz)) * esz;
+    }
+  } else {
+    p.TT = 64;
+    const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
+    p.lds = ((size_t)p.TT * O + (size_t)rows_in * C) * 4;
+  }
+  // chunk so that the grid has ~1024 workgroups, each at least one sub-tile
+  long long target = 1024;
+  long long per_item = (target + B - 1) / B;
+  int ch = (int)((T_out + per_item - 1) / per_item);
+  ch = ((ch + p.TT - 1) / p.TT) * p.TT;
+  if (ch < p.TT) ch = p.TT;
+  p.CH = ch;
+  p.nchunk = (T_out + ch - 1) / ch;
+  p.nwg = p.nchunk * B;
+  p.E = K * C * O + O;
+  p.ws_bytes = (size_t)p.nwg * p.E * sizeof(float);
+  return p;
+}
+
+template <class T, int C, int O, int TT>
+static int launch_wgrad_mfma_t(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds((const void*)wgrad_mfma_kernel<T, C, O, TT>, p.lds, &lds_set, "wgrad_mfma_kernel");
+  if (rc != VQA_OK) return rc;
+  hipLaunchKernelGGL((wgrad_mfma_kernel<T, C, O, TT>), dim3(p.nchunk, a.B), dim3(256), p.lds, s, a);
+  VQA_LAUNCHED("wgrad_mfma_kernel");
+  return VQA_OK;
+}
+
+template <class T, int C, int O>
+static int launch_wgrad_mfma_co(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+  if (p.TT == 256) return launch_wgrad_mfma_t<T, C, O, 256>(a, p, s);
+  if (p.TT == 128) return launch_wgrad_mfma_t<T, C, O, 128>(a, p, s);
+  return launch_wgrad_mfma_t<T, C, O, 64>(a, p, s);
+}
+
+template <class T>
+static int launch_wgrad_mfma(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+  if (a.C == 32 && a.O == 32) return launch_wgrad_mfma_co<T, 32, 32>(a, p, s);
+  if (a.C == 32 && a.O == 64) return launch_wgrad_mfma_co<T, 32, 64>(a, p, s);
+  if (a.C == 64 && a.O == 32) return launch_wgrad_mfma_co<T, 64, 32>(a, p, s);
+  if (a.C == 64 && a.O == 64) return launch_wgrad_mfma_co<T, 64, 64>(a, p, s);
+  vqa::set_error("wgrad: no MFMA tile for C=%d O=%d", a.C, a.O);
+  return VQA_E_UNSUPPORTED;
+}
+
+template <class TX, class TG>
+static int launch_wgrad_direct(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds((const void*)wgrad_direct_kernel<TX, TG, 64>, p.lds, &lds_set, "wgrad_direct_kernel");
+  if (rc != VQA_OK) return rc;
+  hipLaunchKernelGGL((wgrad_direct_kernel<TX, TG, 64>), dim3(p.nchunk, a.B), dim3(256), p.lds, s, a);
+  VQA_LAUNCHED("wgrad_direct_kernel");
+  return VQA_OK;
+}
+
+int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_in, int T_out, int C, int O, int K,
+              int S, int D, int P, int flags, int dtype, void* ws, size_t ws_bytes, hipStream_t s) {
+  VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
+  VQA_ARG(x && g && dw, "null tensor pointer");
+  VQA_ARG(B > 0 && T_in > 0 && T_out > 0 && C > 0 && O > 0 && K > 0 && S > 0 && D > 0, "non-positive shape");
+  WgradPlan p = plan_wgrad(dtype, B, T_in, T_out, C, O, K, S, D, flags);
+  VQA_ARG(ws && ws_bytes >= p.ws_bytes, "workspace too small: need %zu bytes, got %zu", p.ws_bytes, ws_bytes);
+  VQA_REQUIRE(p.lds <= 160 * 1024, VQA_E_UNSUPPORTED, "wgrad: LDS tile too large (%zu B)", p.lds);
+  VQA_REQUIRE(p.mfma || K * C * O <= 16 * 256, VQA_E_UNSUPPORTED, "wgrad: generic path limited to K*C*O<=4096");
+  VQA_REQUIRE(O <= 256 && 256 % O == 0, VQA_E_UNSUPPORTED, "wgrad: C_out must divide 256");
+  WgradArgs a{x, g, (float*)ws, B, T_in, T_out, C, O, K, S, D, P, p.CH, p.nchunk, flags};
+  int rc;
+  if (p.mfma) {
+    rc = dtype == VQA_BF16 ? launch_wgrad_mfma<bf16>(a, p, s) : launch_wgrad_mfma<float>(a, p, s);
+  } else {
+    const bool xf = dtype == VQA_F32 || (flags & VQA_X_F32);
+    const bool gf = dtype == VQA_F32 || (flags & VQA_Y_F32);
+    if (xf && gf) rc = launch_wgrad_direct<float, float>(a, p, s);
+    else if (xf) rc = launch_wgrad_direct<float, bf16>(a, p, s);
+    else if (gf) rc = launch_wgrad_direct<bf16, float>(a, p, s);
+    else rc = launch_wgrad_direct<bf16, bf16>(a, p, s);
+  }
+  if (rc != VQA_OK) return rc;
+  const int KCO = K * C * O;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((p.E + 255) / 256), dim3(256), 0, s, (const float*)ws, p.nwg,
+                     p.E, KCO, dw, db);
+  VQA_LAUNCHED("reduce_partials_kernel");
+  return VQA_OK;
+}
+
+size_t wgrad_ws(int dtype, int B, int T_in, int T_out, int C, int O, int K, int S, int D, int flags) {
+  return plan_wgrad(dtype, B, T_in, T_out, C, O, K, S, D, flags).ws_bytes;
+}
+
+// column-sum (conv-transpose bias gradient): ws must hold nwg*O floats
+static const int kColsumRows = 2048;
+size_t colsum_ws(long long rows, int O) { return (size_t)((rows + kColsumRows - 1) / kColsumRows) * O * sizeof(float); }
+
+int run_colsum(const void* y, long long rows, int O, float* out, int dtype, void* ws, size_t ws_bytes, hipStream_t s) {
+  VQA_REQUIRE(O <= 256 && 256 % O == 0, VQA_E_UNSUPPORTED, "colsum: O must divide 256");
+  const int nwg = (int)((rows + kColsumRows - 1) / kColsumRows);
+  VQA_ARG(ws && ws_bytes >= (size_t)nwg * O * sizeof(float), "colsum workspace too small");
+  if (dtype == VQA_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, dim3(nwg), dim3(256), 0, s, (const bf16*)y, rows, O, kColsumRows,
+                       (float*)ws);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nwg), dim3(256), 0, s, (const float*)y, rows, O, kColsumRows,
+                       (float*)ws);
+  VQA_LAUNCHED("colsum_partial_kernel");
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((O + 255) / 256), dim3(256), 0, s, (const float*)ws, nwg, O, O, out,
+                     (float*)nullptr);
+  VQA_LAUNCHED("reduce_partials_kernel");
+  return VQA_OK;
+}
+
+}  // namespace vqa
+
+// ================================================================================================
+// C ABI
+using namespace vqa;
+
+extern "C" int vqa_same_out_len(int T_in, int stride) { return (T_in + stride - 1) / stride; }
+extern "C" int vqa_same_pad_left(int T_in, int K, int stride, int dilation) {
+  const int out = (T_in + stride - 1) / stride;
+  const int pad = std::max((out - 1) * stride + (K - 1) * dilation + 1 - T_in, 0);
+  return pad / 2;
+}
+
+extern "C" int vqa_conv1d_fwd(const void* x, const float* w, const float* bias, const void* residual, void* y, int B,
+                              int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation, int pad_left,
+                              int flags, int dtype, vqa_stream_t stream) {
+  VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_fwd: T_out %d != ceil(T_in/stride)", T_out);
+  GatherArgs a{x, w, bias, residual, nullptr, y, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
+               W_DIRECT, K, 0, T_out, flags & (VQA_PRE_RELU | VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32)};
+  return run_gather(a, dtype, (hipStream_t)stream);
+}
+
+// flags for the data-gradient gather: the gather input is dy (y side), output dx (x side)
+static int swap_xy_flags(int flags) {
+  int f = flags & (VQA_POST_MASK | VQA_ADD_RESIDUAL);
+  if (flags & VQA_X_F32) f |= VQA_Y_F32;
+  if (flags & VQA_Y_F32) f |= VQA_X_F32;
+  return f;
+}
+
+extern "C" int vqa_conv1d_bwd_data(const void* dy, const float* w, const void* mask, const void* residual, void* dx,
+                                   int B, int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation,
+                                   int pad_left, int flags, int dtype, vqa_stream_t stream) {
+  VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_data: T_out %d != ceil(T_in/stride)", T_out);
+  const int f = swap_xy_flags(flags);
+  if (stride == 1) {
+    GatherArgs a{dy, w, nullptr, residual, mask, dx, B, T_out, T_in, C_out, C_in, K, 1, dilation,
+                 (K - 1) * dilation - pad_left, W_FLIP_T, K, 0, T_in, f};
+    return run_gather(a, dtype, (hipStream_t)stream);
+  }
+  VQA_REQUIRE(stride == 2 && K == 4 && dilation == 1 && pad_left == 1, VQA_E_UNSUPPORTED,
+              "conv1d_bwd_data: strided data-gradient supports stride 2, K 4, pad_left 1 (got s=%d K=%d d=%d p=%d)",
+              stride, K, dilation, pad_left);
+  GatherArgs a{dy, w, nullptr, residual, mask, dx, B, T_out, T_out, C_out, 2 * C_in, 3, 1, 1, 1,
+               W_PAIR, K, pad_left, T_in, f};
+  return run_gather(a, dtype, (hipStream_t)stream);
+}
+
+extern "C" size_t vqa_conv1d_bwd_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                                                  int dilation, int pad_left, int flags, int dtype) {
+  (void)pad_left;
+  return wgrad_ws(dtype, B, T_in, T_out, C_in, C_out, K, stride, dilation, flags);
+}
+
+extern "C" int vqa_conv1d_bwd_weight(const void* x, const void* dy, float* dw, float* db, int B, int T_in, int T_out,
+                                     int C_in, int C_out, int K, int stride, int dilation, int pad_left, int flags,
+                                     int dtype, void* workspace, size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_weight: T_out %d != ceil(T_in/stride)", T_out);
+  return run_wgrad(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
+                   flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int vqa_conv1d_transpose_fwd(const void* x, const float* w, const float* bias, const void* residual,
+                                        void* y, int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                                        int pad_left, int flags, int dtype, vqa_stream_t stream) {
+  VQA_REQUIRE(stride == 2 && K == 4 && pad_left == 1, VQA_E_UNSUPPORTED,
+              "conv1d_transpose: supports stride 2, K 4, pad_left 1 (got s=%d K=%d p=%d)", stride, K, pad_left);
+  VQA_ARG(T_out == stride * T_in, "conv1d_transpose_fwd: T_out %d != stride*T_in", T_out);
+  GatherArgs a{x, w, bias, residual, nullptr, y, B, T_in, T_in, C_in, 2 * C_out, 3, 1, 1, 1,
+               W_PAIR, K, pad_left, T_out, flags & (VQA_PRE_RELU | VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32)};
+  return run_gather(a, dtype, (hipStream_t)stream);
+}
+
+extern "C" int vqa_conv1d_transpose_bwd_data(const void* dy, const float* w, const void* mask, const void* residual,
+                                             void* dx, int B, int T_in, int T_out, int C_in, int C_out, int K,
+                                             int stride, int pad_left, int flags, int dtype, vqa_stream_t stream) {
+  VQA_REQUIRE(stride == 2 && K == 4 && pad_left == 1, VQA_E_UNSUPPORTED,
+              "conv1d_transpose: supports stride 2, K 4, pad_left 1");
+  VQA_ARG(T_out == stride * T_in, "conv1d_transpose_bwd_data: T_out %d != stride*T_in", T_out);
+  GatherArgs a{dy, w, nullptr, residual, mask, dx, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left,
+               W_DIRECT, K, 0, T_in, swap_xy_flags(flags)};
+  return run_gather(a, dtype, (hipStream_t)stream);
+}
+
+extern "C" size_t vqa_conv1d_transpose_bwd_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K,
+                                                            int stride, int pad_left, int flags, int dtype) {
+  (void)pad_left;
+  const int f = swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32);
+  size_t a = wgrad_ws(dtype, B, T_out, T_in, C_out, C_in, K, stride, 1, f);
+  size_t b = colsum_ws((long long)B * T_out, C_out);
+  return std::max(a, b);
+}
+
+extern "C" int vqa_conv1d_transpose_bwd_weight(const void* x, const void* dy, float* dw, float* db, int B, int T_in,
+                                               int T_out, int C_in, int C_out, int K, int stride, int pad_left,
+                                               int flags, int dtype, void* workspace, size_t ws_bytes,
+                                               vqa_stream_t stream) {
+  VQA_REQUIRE(stride == 2 && K == 4 && pad_left == 1, VQA_E_UNSUPPORTED,
+              "conv1d_transpose: supports stride 2, K 4, pad_left 1");
+  VQA_ARG(T_out == stride * T_in, "conv1d_transpose_bwd_weight: T_out %d != stride*T_in", T_out);
+  // dW[k][co][ci] = sum_i dy[2i + k - 1][co] * x[i][ci]: the gather weight-gradient with dy as input
+  const int f = swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32);
+  int rc = run_wgrad(dy, x, dw, nullptr, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left, f, dtype, workspace,
+                     ws_bytes, (hipStream_t)stream);
+  if (rc != VQA_OK || !db) return rc;
+  return run_colsum(dy, (long long)B * T_out, C_out, db, dtype, workspace, ws_bytes, (hipStream_t)stream);
+}

@@ -1,0 +1,115 @@
+// vqa_runtime.hip — error reporting, losses and the Keras-Adam optimizer kernel (gfx950).
+//
+//   vqa_mse_loss   : keras MeanSquaredError(reduction=NONE) + tf.reduce_mean (vqvae.py:91,125) fused with
+//                    its gradient and the spectral-loss gradient add.
+//   vqa_adam_keras : keras.optimizers.Adam() defaults as applied by TF's ApplyAdam (vqvae.py:144,362):
+//                    one launch over the flat fp32 parameter buffer of all levels.
+#include "vqa_common.h"
+#include <stdarg.h>
+#include <stdio.h>
+
+namespace vqa {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+__global__ __launch_bounds__(256) void mse_kernel(const float* x, const float* r, const float* extra, float* dr,
+                                                 long long n, float gscale, float* ws) {
+  __shared__ float red[4];
+  float part = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float d = r[i] - x[i];
+    part += d * d;
+    float g = gscale * d;
+    if (extra) g = g + extra[i];
+    dr[i] = g;
+  }
+  const float s = block_sum_256(part, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void mse_reduce_kernel(const float* ws, int n, float scale, float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += ws[i];
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) out[0] = s * scale;
+}
+
+// TF ApplyAdam (training_ops.cc, non-nesterov): alpha = lr*sqrt(1-b2^t)/(1-b1^t);
+// m += (g - m)*(1-b1); v += (g*g - v)*(1-b2); var -= (m*alpha)/(sqrt(v) + eps).
+__global__ __launch_bounds__(256) void adam_kernel(float* w, const float* g, float* m, float* v, long long n,
+                                                  const int64_t* step, float lr, float b1, float b2, float eps,
+                                                  float gs) {
+  const float t = (float)(step[0] + 1);
+  const float b1p = powf(b1, t), b2p = powf(b2, t);
+  const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float omb1 = 1.f - b1, omb2 = 1.f - b2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gs;
+    float mi = m[i], vi = v[i];
+    mi = mi + (gi - mi) * omb1;
+    vi = vi + (gi * gi - vi) * omb2;
+    m[i] = mi;
+    v[i] = vi;
+    w[i] = w[i] - (mi * alpha) / (sqrtf(vi) + eps);
+  }
+}
+
+__global__ void counter_add_kernel(int64_t* c, int64_t delta) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) c[0] += delta;
+}
+
+static int blocks_for(long long n, int cap) {
+  long long b = (n + 255) / 256;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace vqa
+
+using namespace vqa;
+
+extern "C" const char* vqa_get_last_error(void) { return g_err; }
+extern "C" const char* vqa_version(void) { return "libvqa 0.1 gfx950"; }
+
+extern "C" size_t vqa_mse_loss_workspace(int64_t n) { return (size_t)blocks_for(n, 1024) * sizeof(float); }
+
+extern "C" int vqa_mse_loss(const float* x, const float* r, const float* extra_grad, float* dr, float* loss_out,
+                            int64_t n, void* workspace, size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(x && r && dr && loss_out && n > 0, "mse_loss: bad arguments");
+  const int nb = blocks_for(n, 1024);
+  VQA_ARG(workspace && ws_bytes >= (size_t)nb * sizeof(float), "mse_loss: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const float inv_n = (float)(1.0 / (double)n);
+  const float gscale = (float)(2.0 / (double)n);
+  hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(256), 0, s, x, r, extra_grad, dr, (long long)n, gscale,
+                     (float*)workspace);
+  VQA_LAUNCHED("mse_kernel");
+  hipLaunchKernelGGL(mse_reduce_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, inv_n, loss_out);
+  VQA_LAUNCHED("mse_reduce_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, const int64_t* step, float lr,
+                              float beta1, float beta2, float eps, float grad_scale, vqa_stream_t stream) {
+  VQA_ARG(w && g && m && v && step && n > 0, "adam: bad arguments");
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n, 4096)), dim3(256), 0, (hipStream_t)stream, w, g, m, v,
+                     (long long)n, step, lr, beta1, beta2, eps, grad_scale);
+  VQA_LAUNCHED("adam_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_counter_add(int64_t* counter, int64_t delta, vqa_stream_t stream) {
+  VQA_ARG(counter, "counter_add: null pointer");
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, delta);
+  VQA_LAUNCHED("counter_add_kernel");
+  return VQA_OK;
+}

@@ -1,0 +1,403 @@
+// vqa_vq.hip — EMA vector quantizer kernels (gfx950).
+//
+// Replaces the TF op sequence of VectorQuantizer.call (VectorQuantizer.py:75-165):
+//   get_code_indices :170-186  -> vq_argmin_mfma_kernel (fp32 MFMA distance tiles + wave argmin);
+//                                 no N x K distance matrix is materialised.
+//   one_hot @ E^T    :86-90    -> a row gather from ET = E^T (K, D) kept by the EMA kernel.
+//   commit loss      :97-99, straight-through :114, EMA sums :123-124 -> vq_quantize_kernel.
+//   EMA + dead-code reset :126-145, metrics :149-159 -> vq_ema_apply_kernel / vq_metrics_kernel.
+// The reset candidates (tf.random.shuffle, :137) use an injected, seeded Feistel permutation.
+#include "vqa_common.h"
+
+namespace vqa {
+
+// ---- argmin -------------------------------------------------------------------------------------
+// One workgroup = 4 waves x 32 rows. Distances d = (|z|^2 + |e|^2) - 2 z.e exactly as the reference
+// orders them (VectorQuantizer.py:175-182), in fp32; z.e on v_mfma_f32_16x16x4_f32 (an exact fp32
+// FMA chain over d). Codebook chunks of 128 codes are staged through LDS and shared by the waves.
+template <class T, int D>
+__global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const float* E, const float* esq,
+                                                            int64_t* idx, float* mind, long long N, int K) {
+  constexpr int KC = 128, DS = D / 4, RT = 2;
+  __shared__ float El[D * KC];
+  __shared__ float el2[KC];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long n0 = (long long)blockIdx.x * 128 + wave * 32;
+
+  // A fragments: z[n0 + rt*16 + (lane&15)][4*ds + (lane>>4)]
+  float af[RT][DS];
+  float zsq[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const long long row = n0 + rt * 16 + (lane & 15);
+    float s = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      const float v = row < N ? ld(z + row * D + 4 * ds + (lane >> 4)) : 0.f;
+      af[rt][ds] = v;
+      s += v * v;
+    }
+    // full row |z|^2 lives in the 4 lanes {l, l^16, l^32, l^48}
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    zsq[rt] = s;
+  }
+  // accumulator lane holds rows 4*(lane>>4)+r: fetch their |z|^2 from lane (4*(lane>>4)+r)
+  float zq[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(zsq[rt], 4 * (lane >> 4) + r, 64);
+
+  float best[RT][4];
+  int bidx[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      best[rt][r] = __builtin_inff();
+      bidx[rt][r] = 0x7fffffff;
+    }
+
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < D * KC; e += 256) {
+      const int d = e / KC, kk = e - d * KC;
+      El[e] = (k0 + kk < K) ? E[(long long)d * K + k0 + kk] : 0.f;
+    }
+    for (int e = threadIdx.x; e < KC; e += 256) el2[e] = (k0 + e < K) ? esq[k0 + e] : 0.f;
+    __syncthreads();
+#pragma unroll 1
+    for (int ct = 0; ct < KC / 16; ++ct) {
+      const int kl = ct * 16 + (lane & 15);
+      float bf[DS];
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) bf[ds] = El[(4 * ds + (lane >> 4)) * KC + kl];
+      const int kg = k0 + kl;
+      const float e2 = el2[kl];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ds = 0; ds < DS; ++ds) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt][ds], bf[ds], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = zq[rt][r] + e2;
+          const float dist = t - 2.0f * acc[r];
+          if (kg < K && dist < best[rt][r]) {
+            best[rt][r] = dist;
+            bidx[rt][r] = kg;
+          }
+        }
+      }
+    }
+  }
+  // reduce over the 16 lanes holding the same rows (lane bits 0..3), ties -> lowest index
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float b = best[rt][r];
+      int bi = bidx[rt][r];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        const float ob = __shfl_xor(b, m, 64);
+        const int oi = __shfl_xor(bi, m, 64);
+        if (ob < b || (ob == b && oi < bi)) {
+          b = ob;
+          bi = oi;
+        }
+      }
+      const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
+      if ((lane & 15) == 0 && row < N) {
+        idx[row] = bi;
+        if (mind) mind[row] = b;
+      }
+    }
+}
+
+// generic argmin (any D): one thread per row
+template <class T>
+__global__ __launch_bounds__(256) void vq_argmin_direct_kernel(const T* z, const float* E, const float* esq,
+                                                              int64_t* idx, float* mind, long long N, int D, int K) {
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float zsq = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float v = ld(z + n * D + d);
+    zsq += v * v;
+  }
+  float best = __builtin_inff();
+  int bi = 0;
+  for (int k = 0; k < K; ++k) {
+    float dot = 0.f;
+    for (int d = 0; d < D; ++d) dot += ld(z + n * D + d) * E[(long long)d * K + k];
+    const float t = zsq + esq[k];
+    const float dist = t - 2.0f * dot;
+    if (dist < best) {
+      best = dist;
+      bi = k;
+    }
+  }
+  idx[n] = bi;
+  if (mind) mind[n] = best;
+}
+
+__global__ __launch_bounds__(256) void vq_sqnorm_kernel(const float* E, float* esq, int D, int K) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float v = E[(long long)d * K + k];
+    s += v * v;
+  }
+  esq[k] = s;
+}
+
+// ---- quantize / straight-through / commitment / EMA sums ----------------------------------------
+// thread per (row, d); partial sums of (q - z)^2 per workgroup -> ws
+template <class T>
+__global__ __launch_bounds__(256) void vq_quantize_kernel(const T* z, const float* ET, const int64_t* idx, T* qst,
+                                                         float* m_sumT, float* n_sum, long long N, int D,
+                                                         float* ws) {
+  __shared__ float red[4];
+  const long long total = N * D;
+  float part = 0.f;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long n = e / D;
+    const int d = (int)(e - n * D);
+    const long long k = idx[n];
+    const float zf = ld(z + e);
+    const float q = ET[k * D + d];
+    const float diff = q - zf;
+    part += diff * diff;
+    st(qst + e, zf + diff);
+    if (m_sumT) {
+      atomicAdd(m_sumT + k * D + d, zf);
+      if (d == 0) atomicAdd(n_sum + k, 1.0f);
+    }
+  }
+  const float s = block_sum_256(part, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+// out[0] = scale * sum(ws[0..n))  (single workgroup, fixed order)
+__global__ __launch_bounds__(256) void reduce_scalar_kernel(const float* ws, int n, float scale, float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += ws[i];
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) out[0] = s * scale;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void vq_backward_kernel(const T* dq, const T* z, const float* ET,
+                                                         const int64_t* idx, T* dz, float scale, long long N, int D) {
+  const long long total = N * D;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long n = e / D;
+    const int d = (int)(e - n * D);
+    const float zf = ld(z + e);
+    const float q = ET[idx[n] * D + d];
+    st(dz + e, ld(dq + e) + scale * (zf - q));
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void vq_reset_rows_kernel(const T* z, float* RT, long long N_local,
+                                                           long long row_offset, long long N_global, int D, int K,
+                                                           uint64_t seed, const int64_t* counter, int level) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)K * D) return;
+  const int k = (int)(e / D), d = (int)(e - (long long)k * D);
+  const long long M = N_global >= K ? N_global : N_global * ((K + N_global - 1) / N_global);
+  const uint64_t key = perm_key(seed, counter[0], level);
+  const long long g = perm_index(key, M, k) % N_global;
+  const long long loc = g - row_offset;
+  RT[e] = (loc >= 0 && loc < N_local) ? ld(z + loc * D + d) : 0.f;
+}
+
+// one wave per code, lane = d (D <= 64)
+__global__ __launch_bounds__(256) void vq_ema_apply_kernel(float* E, float* ET, float* m_t, float* N_t,
+                                                          const float* m_sumT, const float* n_sum, const float* RT,
+                                                          float g, float omg, float thresh, int64_t* counter, int D,
+                                                          int K) {
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int d = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;
+  if (k >= K || d >= D) return;
+  // TF: gamma * N_t + (1 - gamma) * N_t_  — two products then a sum (no contraction: -ffp-contract=off)
+  const float Nn = g * N_t[k] + omg * n_sum[k];
+  const float mn = g * m_t[(long long)d * K + k] + omg * m_sumT[(long long)k * D + d];
+  const bool use = Nn >= thresh;
+  const float Nc = fminf(fmaxf(Nn, 1e-8f), 1e8f);
+  const float e = use ? mn / Nc : RT[(long long)k * D + d];
+  m_t[(long long)d * K + k] = mn;
+  E[(long long)d * K + k] = e;
+  ET[(long long)k * D + d] = e;
+  if (d == 0) N_t[k] = Nn;
+}
+
+// metrics: [0] #(n_sum >= thr), [1] #(N_t >= thr), [2] -sum p log(p + 1e-8), p = n_sum / sum(n_sum)
+__global__ __launch_bounds__(256) void vq_metrics_kernel(const float* n_sum, const float* N_t, float thresh, int K,
+                                                        float* metrics) {
+  __shared__ float red[4];
+  float tot = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) tot += n_sum[k];
+  tot = block_sum_256(tot, red);
+  float bu = 0.f, ru = 0.f, ent = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float c = n_sum[k];
+    bu += c >= thresh ? 1.f : 0.f;
+    ru += N_t[k] >= thresh ? 1.f : 0.f;
+    const float p = c / tot;
+    ent += p * logf(p + 1e-8f);
+  }
+  __syncthreads();
+  bu = block_sum_256(bu, red);
+  __syncthreads();
+  ru = block_sum_256(ru, red);
+  __syncthreads();
+  ent = block_sum_256(ent, red);
+  if (threadIdx.x == 0) {
+    metrics[0] = bu;
+    metrics[1] = ru;
+    metrics[2] = -ent;
+  }
+}
+
+static int quantize_blocks(long long total) {
+  long long b = (total + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace vqa
+
+using namespace vqa;
+
+extern "C" int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream) {
+  VQA_ARG(E && e_sqnorm && D > 0 && K > 0, "vq_sqnorm: bad arguments");
+  hipLaunchKernelGGL(vq_sqnorm_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, E, e_sqnorm, D, K);
+  VQA_LAUNCHED("vq_sqnorm_kernel");
+  return VQA_OK;
+}
+
+template <class T>
+static int launch_argmin(const void* z, const float* E, const float* esq, int64_t* idx, float* mind, long long N,
+                         int D, int K, hipStream_t s) {
+  const dim3 g((unsigned)((N + 127) / 128));
+  switch (D) {
+    case 4: hipLaunchKernelGGL((vq_argmin_mfma_kernel<T, 4>), g, dim3(256), 0, s, (const T*)z, E, esq, idx, mind, N, K); break;
+    case 8: hipLaunchKernelGGL((vq_argmin_mfma_kernel<T, 8>), g, dim3(256), 0, s, (const T*)z, E, esq, idx, mind, N, K); break;
+    case 16: hipLaunchKernelGGL((vq_argmin_mfma_kernel<T, 16>), g, dim3(256), 0, s, (const T*)z, E, esq, idx, mind, N, K); break;
+    case 32: hipLaunchKernelGGL((vq_argmin_mfma_kernel<T, 32>), g, dim3(256), 0, s, (const T*)z, E, esq, idx, mind, N, K); break;
+    case 64: hipLaunchKernelGGL((vq_argmin_mfma_kernel<T, 64>), g, dim3(256), 0, s, (const T*)z, E, esq, idx, mind, N, K); break;
+    default:
+      hipLaunchKernelGGL(vq_argmin_direct_kernel<T>, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, (const T*)z, E,
+                         esq, idx, mind, N, D, K);
+  }
+  VQA_LAUNCHED("vq_argmin");
+  return VQA_OK;
+}
+
+extern "C" int vqa_vq_argmin(const void* z, const float* E, const float* e_sqnorm, int64_t* idx, float* min_dist,
+                             int64_t N, int D, int K, int dtype, vqa_stream_t stream) {
+  VQA_ARG(z && E && e_sqnorm && idx, "vq_argmin: null pointer");
+  VQA_ARG(N > 0 && D > 0 && K > 0, "vq_argmin: bad shape N=%lld D=%d K=%d", (long long)N, D, K);
+  VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "vq_argmin: unknown dtype %d", dtype);
+  if (dtype == VQA_BF16) return launch_argmin<bf16>(z, E, e_sqnorm, idx, min_dist, N, D, K, (hipStream_t)stream);
+  return launch_argmin<float>(z, E, e_sqnorm, idx, min_dist, N, D, K, (hipStream_t)stream);
+}
+
+extern "C" size_t vqa_vq_quantize_workspace(int64_t N, int D, int K, int dtype) {
+  (void)K;
+  (void)dtype;
+  return (size_t)quantize_blocks((long long)N * D) * sizeof(float);
+}
+
+extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* idx, void* q_st, float* commit_out,
+                               float* m_sumT, float* n_sum, int64_t N, int D, int K, float beta, int dtype,
+                               void* workspace, size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(z && ET && idx && q_st && commit_out, "vq_quantize: null pointer");
+  VQA_ARG(!m_sumT == !n_sum, "vq_quantize: m_sumT and n_sum must both be set or both NULL");
+  VQA_ARG(N > 0 && D > 0 && K > 0, "vq_quantize: bad shape");
+  const int nb = quantize_blocks((long long)N * D);
+  VQA_ARG(workspace && ws_bytes >= (size_t)nb * sizeof(float), "vq_quantize: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQA_BF16)
+    hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st,
+                       m_sumT, n_sum, (long long)N, D, (float*)workspace);
+  else if (dtype == VQA_F32)
+    hipLaunchKernelGGL(vq_quantize_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)z, ET, idx, (float*)q_st,
+                       m_sumT, n_sum, (long long)N, D, (float*)workspace);
+  else
+    VQA_ARG(false, "vq_quantize: unknown dtype %d", dtype);
+  VQA_LAUNCHED("vq_quantize_kernel");
+  // beta * mean((q - z)^2) over N*D elements (VectorQuantizer.py:97-99)
+  const float scale = (float)((double)beta / ((double)N * (double)D));
+  hipLaunchKernelGGL(reduce_scalar_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, scale, commit_out);
+  VQA_LAUNCHED("reduce_scalar_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_vq_backward(const void* dq, const void* z, const float* ET, const int64_t* idx, void* dz,
+                               float scale, int64_t N, int D, int dtype, vqa_stream_t stream) {
+  VQA_ARG(dq && z && ET && idx && dz && N > 0 && D > 0, "vq_backward: bad arguments");
+  const int nb = quantize_blocks((long long)N * D);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQA_BF16)
+    hipLaunchKernelGGL(vq_backward_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)dq, (const bf16*)z, ET, idx,
+                       (bf16*)dz, scale, (long long)N, D);
+  else if (dtype == VQA_F32)
+    hipLaunchKernelGGL(vq_backward_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dq, (const float*)z, ET,
+                       idx, (float*)dz, scale, (long long)N, D);
+  else
+    VQA_ARG(false, "vq_backward: unknown dtype %d", dtype);
+  VQA_LAUNCHED("vq_backward_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_vq_reset_rows(const void* z, float* RT, int64_t N_local, int64_t row_offset, int64_t N_global,
+                                 int D, int K, uint64_t seed, const int64_t* counter, int level, int dtype,
+                                 vqa_stream_t stream) {
+  VQA_ARG(z && RT && counter && N_local > 0 && N_global >= N_local && D > 0 && K > 0, "vq_reset_rows: bad arguments");
+  VQA_ARG(row_offset >= 0 && row_offset + N_local <= N_global, "vq_reset_rows: bad row range");
+  const long long total = (long long)K * D;
+  const dim3 g((unsigned)((total + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQA_BF16)
+    hipLaunchKernelGGL(vq_reset_rows_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)z, RT, (long long)N_local,
+                       (long long)row_offset, (long long)N_global, D, K, seed, counter, level);
+  else if (dtype == VQA_F32)
+    hipLaunchKernelGGL(vq_reset_rows_kernel<float>, g, dim3(256), 0, s, (const float*)z, RT, (long long)N_local,
+                       (long long)row_offset, (long long)N_global, D, K, seed, counter, level);
+  else
+    VQA_ARG(false, "vq_reset_rows: unknown dtype %d", dtype);
+  VQA_LAUNCHED("vq_reset_rows_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_vq_ema_apply(float* E, float* ET, float* m_t, float* N_t, const float* m_sumT, const float* n_sum,
+                                const float* RT, float gamma, float one_minus_gamma, float thresh, float* metrics,
+                                int64_t* counter, int D, int K, vqa_stream_t stream) {
+  VQA_ARG(E && ET && m_t && N_t && m_sumT && n_sum && RT && counter, "vq_ema_apply: null pointer");
+  VQA_ARG(D > 0 && D <= 64 && K > 0, "vq_ema_apply: supports D <= 64 (got D=%d)", D);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(vq_ema_apply_kernel, dim3((K + 3) / 4), dim3(256), 0, s, E, ET, m_t, N_t, m_sumT, n_sum, RT, gamma,
+                     one_minus_gamma, thresh, counter, D, K);
+  VQA_LAUNCHED("vq_ema_apply_kernel");
+  if (metrics) {
+    hipLaunchKernelGGL(vq_metrics_kernel, dim3(1), dim3(256), 0, s, n_sum, (const float*)N_t, thresh, K, metrics);
+    VQA_LAUNCHED("vq_metrics_kernel");
+  }
+  return VQA_OK;
+}
+
+extern "C" int64_t vqa_reset_perm_index(uint64_t seed, int64_t counter, int level, int64_t M, int64_t k) {
+  if (M <= 0 || k < 0 || k >= M) return -1;
+  return perm_index(perm_key(seed, counter, level), M, k);
+}

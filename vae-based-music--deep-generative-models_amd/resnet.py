@@ -1,0 +1,72 @@
+"""Dilated residual stacks — drop-in for the reference resnet.py (ResnetConv1DBlock, DilatedResnet1D).
+
+resnet.py:7-29   ResnetConv1DBlock: y = x + Conv1D_k3,d1(ReLU(Conv1D_k3,dil(ReLU(x))))
+resnet.py:40-59  DilatedResnet1D: `depth` blocks, dilation dilation_factor**d (or **(d % dilation_cycle)),
+                 reversed for decoders.
+Both convs run on the HIP gather-conv kernel with the ReLUs fused into the LDS staging of the input and
+the residual add fused into the epilogue; the backward fuses ReLU' masks and the residual gradient.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+from vqa_layers import Conv1D
+from vqa_module import Layer
+
+
+class ResnetConv1DBlock(Layer):
+    def __init__(self, input_dim, filters, dilation=1, **kwargs):
+        super().__init__(**kwargs)
+        self.input_dim, self.filters, self.dilation = input_dim, filters, dilation
+        self._saved = None
+
+    def _build(self, store, prefix, input_dim):
+        assert input_dim == self.input_dim, f"{prefix}: input_dim {input_dim} != {self.input_dim}"
+        self.conv_a = Conv1D(store, f"{prefix}/conv_a", self.input_dim, self.filters, 3, 1, self.dilation)
+        self.conv_b = Conv1D(store, f"{prefix}/conv_b", self.filters, self.input_dim, 3, 1, 1)
+        return self.input_dim
+
+    def forward(self, x, save=False):
+        h = self.conv_a.forward(x, self.cdt, pre_relu=True)
+        y = self.conv_b.forward(h, self.cdt, pre_relu=True, residual=x)
+        self._saved = (x, h) if save else None
+        return y
+
+    def backward(self, dy):
+        x, h = self._saved
+        self._saved = None
+        T = x.shape[1]
+        dh = self.conv_b.backward_data(dy, T, self.cdt, mask=h)
+        self.conv_b.backward_weight(h, dy, self.cdt, pre_relu=True)
+        dx = self.conv_a.backward_data(dh, T, self.cdt, mask=x, residual=dy)
+        self.conv_a.backward_weight(x, dh, self.cdt, pre_relu=True)
+        return dx
+
+
+class DilatedResnet1D(Layer):
+    def __init__(self, input_dim, depth, dilation_factor=1, reverse_dilation=False, dilation_cycle=None, **kwargs):
+        super().__init__(**kwargs)
+        self.input_dim, self.depth = input_dim, depth
+
+        def _get_dilation(d):  # resnet.py:44-48
+            return dilation_factor ** d if dilation_cycle is None else dilation_factor ** (d % dilation_cycle)
+
+        self.dilations: List[int] = [_get_dilation(d) for d in range(depth)]
+        if reverse_dilation:  # resnet.py:54-55
+            self.dilations = self.dilations[::-1]
+        self.blocks = [ResnetConv1DBlock(input_dim, input_dim, dilation=d) for d in self.dilations]
+
+    def _build(self, store, prefix, input_dim):
+        for j, blk in enumerate(self.blocks):
+            blk.build(store, f"{prefix}/rb{j}", input_dim, self.cdt)
+        return input_dim
+
+    def forward(self, x, save=False):
+        for blk in self.blocks:
+            x = blk.forward(x, save)
+        return x
+
+    def backward(self, dy):
+        for blk in reversed(self.blocks):
+            dy = blk.backward(dy)
+        return dy

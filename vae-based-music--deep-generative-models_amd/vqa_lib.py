@@ -1,0 +1,224 @@
+"""ctypes binding of libvqa.so (the C-ABI in include/vqa.h).
+
+There is no CPU or PyTorch fallback: if libvqa.so is missing, `lib()` raises ImportError, and every op
+raises VQAError with the library's own message when a call fails. Tensors are passed as raw device
+pointers on torch's current HIP stream (so the calls are captured by torch.cuda.graph).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvqa.so")
+
+F32, BF16 = 0, 1
+PRE_RELU, ADD_RESIDUAL, POST_MASK, X_F32, Y_F32 = 1, 2, 4, 8, 16
+
+EXPORTED = [
+    "vqa_get_last_error", "vqa_version", "vqa_same_pad_left", "vqa_same_out_len",
+    "vqa_conv1d_fwd", "vqa_conv1d_bwd_data", "vqa_conv1d_bwd_weight", "vqa_conv1d_bwd_weight_workspace",
+    "vqa_conv1d_transpose_fwd", "vqa_conv1d_transpose_bwd_data", "vqa_conv1d_transpose_bwd_weight",
+    "vqa_conv1d_transpose_bwd_weight_workspace",
+    "vqa_vq_sqnorm", "vqa_vq_argmin", "vqa_vq_quantize", "vqa_vq_quantize_workspace", "vqa_vq_backward",
+    "vqa_vq_reset_rows", "vqa_vq_ema_apply", "vqa_reset_perm_index",
+    "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_counter_add",
+]
+
+
+class VQAError(RuntimeError):
+    pass
+
+
+_P, _I, _L, _S, _F, _U = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float,
+                          ctypes.c_uint64)
+_CONV = [_I] * 11  # B T_in T_out C_in C_out K stride dilation pad flags dtype
+_CONVT = [_I] * 10  # B T_in T_out C_in C_out K stride pad flags dtype
+
+_SIGS = {
+    "vqa_get_last_error": (ctypes.c_char_p, []),
+    "vqa_version": (ctypes.c_char_p, []),
+    "vqa_same_pad_left": (_I, [_I, _I, _I, _I]),
+    "vqa_same_out_len": (_I, [_I, _I]),
+    "vqa_conv1d_fwd": (_I, [_P, _P, _P, _P, _P] + _CONV + [_P]),
+    "vqa_conv1d_bwd_data": (_I, [_P, _P, _P, _P, _P] + _CONV + [_P]),
+    "vqa_conv1d_bwd_weight": (_I, [_P, _P, _P, _P] + _CONV + [_P, _S, _P]),
+    "vqa_conv1d_bwd_weight_workspace": (_S, _CONV),
+    "vqa_conv1d_transpose_fwd": (_I, [_P, _P, _P, _P, _P] + _CONVT + [_P]),
+    "vqa_conv1d_transpose_bwd_data": (_I, [_P, _P, _P, _P, _P] + _CONVT + [_P]),
+    "vqa_conv1d_transpose_bwd_weight": (_I, [_P, _P, _P, _P] + _CONVT + [_P, _S, _P]),
+    "vqa_conv1d_transpose_bwd_weight_workspace": (_S, _CONVT),
+    "vqa_vq_sqnorm": (_I, [_P, _P, _I, _I, _P]),
+    "vqa_vq_argmin": (_I, [_P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "vqa_vq_quantize": (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _F, _I, _P, _S, _P]),
+    "vqa_vq_quantize_workspace": (_S, [_L, _I, _I, _I]),
+    "vqa_vq_backward": (_I, [_P, _P, _P, _P, _P, _F, _L, _I, _I, _P]),
+    "vqa_vq_reset_rows": (_I, [_P, _P, _L, _L, _L, _I, _I, _U, _P, _I, _I, _P]),
+    "vqa_vq_ema_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P, _I, _I, _P]),
+    "vqa_reset_perm_index": (_L, [_U, _L, _I, _L, _L]),
+    "vqa_mse_loss": (_I, [_P, _P, _P, _P, _P, _L, _P, _S, _P]),
+    "vqa_mse_loss_workspace": (_S, [_L]),
+    "vqa_adam_keras": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P]),
+    "vqa_counter_add": (_I, [_P, _L, _P]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libvqa.so once. Raises ImportError if it has not been built (no fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libvqa.so not found at {LIB_PATH}; build it with `python -c "
+                              f"'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().vqa_get_last_error().decode()
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise VQAError(f"{what} failed ({rc}): {last_error()}")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise VQAError("libvqa ops take device tensors only (got a CPU tensor)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.bfloat16:
+        return BF16
+    if dt == torch.float32:
+        return F32
+    raise VQAError(f"unsupported activation dtype {dt}")
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ---- host-only helpers (callable without a GPU) --------------------------------------------------
+def same_pad_left(T_in: int, K: int, stride: int, dilation: int = 1) -> int:
+    return lib().vqa_same_pad_left(T_in, K, stride, dilation)
+
+
+def same_out_len(T_in: int, stride: int) -> int:
+    return lib().vqa_same_out_len(T_in, stride)
+
+
+def reset_perm_index(seed: int, counter: int, level: int, M: int, k: int) -> int:
+    return lib().vqa_reset_perm_index(seed, counter, level, M, k)
+
+
+# ---- device ops ------------------------------------------------------------------------------------
+def conv1d_fwd(x, w, b, residual, y, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype):
+    _check(lib().vqa_conv1d_fwd(ptr(x), ptr(w), ptr(b), ptr(residual), ptr(y), B, T_in, T_out, C_in, C_out, K,
+                                stride, dilation, pad, flags, dtype, stream()), "vqa_conv1d_fwd")
+
+
+def conv1d_bwd_data(dy, w, mask, residual, dx, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype):
+    _check(lib().vqa_conv1d_bwd_data(ptr(dy), ptr(w), ptr(mask), ptr(residual), ptr(dx), B, T_in, T_out, C_in,
+                                     C_out, K, stride, dilation, pad, flags, dtype, stream()), "vqa_conv1d_bwd_data")
+
+
+def conv1d_bwd_weight(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype):
+    n = lib().vqa_conv1d_bwd_weight_workspace(B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype)
+    ws = workspace(n, x.device)
+    _check(lib().vqa_conv1d_bwd_weight(ptr(x), ptr(dy), ptr(dw), ptr(db), B, T_in, T_out, C_in, C_out, K, stride,
+                                       dilation, pad, flags, dtype, ptr(ws), ws.numel(), stream()),
+           "vqa_conv1d_bwd_weight")
+
+
+def conv1d_transpose_fwd(x, w, b, residual, y, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype):
+    _check(lib().vqa_conv1d_transpose_fwd(ptr(x), ptr(w), ptr(b), ptr(residual), ptr(y), B, T_in, T_out, C_in,
+                                          C_out, K, stride, pad, flags, dtype, stream()), "vqa_conv1d_transpose_fwd")
+
+
+def conv1d_transpose_bwd_data(dy, w, mask, residual, dx, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype):
+    _check(lib().vqa_conv1d_transpose_bwd_data(ptr(dy), ptr(w), ptr(mask), ptr(residual), ptr(dx), B, T_in, T_out,
+                                               C_in, C_out, K, stride, pad, flags, dtype, stream()),
+           "vqa_conv1d_transpose_bwd_data")
+
+
+def conv1d_transpose_bwd_weight(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype):
+    n = lib().vqa_conv1d_transpose_bwd_weight_workspace(B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype)
+    ws = workspace(n, x.device)
+    _check(lib().vqa_conv1d_transpose_bwd_weight(ptr(x), ptr(dy), ptr(dw), ptr(db), B, T_in, T_out, C_in, C_out, K,
+                                                 stride, pad, flags, dtype, ptr(ws), ws.numel(), stream()),
+           "vqa_conv1d_transpose_bwd_weight")
+
+
+def vq_sqnorm(E, esq):
+    D, K = E.shape
+    _check(lib().vqa_vq_sqnorm(ptr(E), ptr(esq), D, K, stream()), "vqa_vq_sqnorm")
+
+
+def vq_argmin(z, E, esq, idx, min_dist=None):
+    N, D = z.shape
+    K = E.shape[1]
+    _check(lib().vqa_vq_argmin(ptr(z), ptr(E), ptr(esq), ptr(idx), ptr(min_dist), N, D, K, dtype_code(z.dtype),
+                               stream()), "vqa_vq_argmin")
+
+
+def vq_quantize(z, ET, idx, q_st, commit_out, m_sumT, n_sum, beta):
+    N, D = z.shape
+    K = ET.shape[0]
+    dt = dtype_code(z.dtype)
+    ws = workspace(lib().vqa_vq_quantize_workspace(N, D, K, dt), z.device)
+    _check(lib().vqa_vq_quantize(ptr(z), ptr(ET), ptr(idx), ptr(q_st), ptr(commit_out), ptr(m_sumT), ptr(n_sum), N,
+                                 D, K, beta, dt, ptr(ws), ws.numel(), stream()), "vqa_vq_quantize")
+
+
+def vq_backward(dq, z, ET, idx, dz, scale):
+    N, D = z.shape
+    _check(lib().vqa_vq_backward(ptr(dq), ptr(z), ptr(ET), ptr(idx), ptr(dz), scale, N, D, dtype_code(z.dtype),
+                                 stream()), "vqa_vq_backward")
+
+
+def vq_reset_rows(z, RT, row_offset, N_global, seed, counter, level):
+    N, D = z.shape
+    K = RT.shape[0]
+    _check(lib().vqa_vq_reset_rows(ptr(z), ptr(RT), N, row_offset, N_global, D, K, seed, ptr(counter), level,
+                                   dtype_code(z.dtype), stream()), "vqa_vq_reset_rows")
+
+
+def vq_ema_apply(E, ET, m_t, N_t, m_sumT, n_sum, RT, gamma, omg, thresh, metrics, counter):
+    D, K = E.shape
+    _check(lib().vqa_vq_ema_apply(ptr(E), ptr(ET), ptr(m_t), ptr(N_t), ptr(m_sumT), ptr(n_sum), ptr(RT), gamma, omg,
+                                  thresh, ptr(metrics), ptr(counter), D, K, stream()), "vqa_vq_ema_apply")
+
+
+def mse_loss(x, r, extra, dr, loss_out):
+    n = x.numel()
+    ws = workspace(lib().vqa_mse_loss_workspace(n), x.device)
+    _check(lib().vqa_mse_loss(ptr(x), ptr(r), ptr(extra), ptr(dr), ptr(loss_out), n, ptr(ws), ws.numel(), stream()),
+           "vqa_mse_loss")
+
+
+def adam_keras(w, g, m, v, step, lr, beta1, beta2, eps, grad_scale):
+    _check(lib().vqa_adam_keras(ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), ptr(step), lr, beta1, beta2, eps,
+                                grad_scale, stream()), "vqa_adam_keras")
+
+
+def counter_add(counter, delta=1):
+    _check(lib().vqa_counter_add(ptr(counter), delta, stream()), "vqa_counter_add")

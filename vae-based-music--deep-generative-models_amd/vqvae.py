@@ -1,0 +1,390 @@
+"""Multi-level VQ-VAE — drop-in for the reference vqvae.py (VQVAE, get_vqvae).
+
+vqvae.py:30-91    VQVAE(input_shape, levels, latent_dim, down_depth, strides, num_embeddings=128,
+                  residual_width=64, residual_depth=4, dilation_factor=1, train_variance=1.0): `levels`
+                  independent {Encoder(depth=l+1), VectorQuantizer, Decoder(depth=l+1)} on the waveform.
+vqvae.py:111-146  train_step: per level recon MSE + commitment + multispectral loss, summed; gradients of
+                  all levels' conv weights; Adam.
+vqvae.py:148-172  test_step (the VQ keeps its default training=True, so the EMA runs — kept on purpose).
+vqvae.py:178-206  call(x, training=False) -> (recons, loss lists).
+vqvae.py:208-260  encode / encode_level / decode / decode_level.
+vqvae.py:262-304  update_metrics (running means; key names kept).
+
+MI355X design: every conv / VQ / loss / optimizer op is a libvqa HIP kernel called through the C-ABI on
+torch's current stream; the backward is written out explicitly (no autograd tape over the conv stack);
+each level runs forward then backward immediately (levels are independent), so only one level's
+activations are alive. Weights, gradients and the codebook EMA sums are flat fp32 buffers: the whole
+data-parallel exchange is ONE all_reduce (RCCL over xGMI) of [grads | EMA sums | reset rows | losses].
+`capture_train_step` records the full step as a hipGraph (torch.cuda.graph) so replay has no host cost.
+"""
+from __future__ import annotations
+
+from itertools import chain
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import vqa_lib as V
+from data_utils import SpectralTarget, multispectral_loss_and_grad
+from encdec import Decoder, Encoder
+from vqa_layers import ParamStore
+from vqa_metrics import Mean
+from vqa_optim import Adam
+from VectorQuantizer import VectorQuantizer
+
+
+def _dtype(d) -> torch.dtype:
+    if d in ("bf16", "bfloat16", torch.bfloat16):
+        return torch.bfloat16
+    if d in ("fp32", "float32", torch.float32):
+        return torch.float32
+    raise ValueError(f"unsupported compute dtype {d}")
+
+
+class _LevelModel:
+    """Stands in for the per-level keras.Model of get_vqvae (vqvae.py:15-21): x -> enc -> vq -> dec."""
+
+    def __init__(self, owner: "VQVAE", level: int):
+        self.owner, self.level = owner, level
+        self.name = f"vq_vae_{level}"
+
+    def __call__(self, x, training=True):
+        return self.owner._level_forward_only(self.owner._as_input(x), self.level, training)
+
+    @property
+    def losses(self):
+        return self.owner.vqs[self.level].losses
+
+    @property
+    def trainable_variables(self):
+        o = self.owner
+        return [o.store.view(n) for n, _, _ in o.store.specs if n.startswith((f"enc{self.level}/", f"dec{self.level}/"))]
+
+
+def get_vqvae(input_shape, encoder, decoder, vq, level=0):
+    """vqvae.py:15-21 — provided for API parity; VQVAE builds its levels itself."""
+    raise NotImplementedError("build a VQVAE; its .vqvaes[level] are the per-level models")
+
+
+class VQVAE:
+    def __init__(self, input_shape, levels, latent_dim, down_depth, strides, num_embeddings=128, residual_width=64,
+                 residual_depth=4, dilation_factor=1, train_variance=1.0, *, dtype="bf16", device="cuda",
+                 seed=1, codebook_seed=2, reset_seed=3, process_group=None, name="vqvae", **kwargs):
+        self.input_shape = tuple(input_shape)
+        self.T = int(self.input_shape[0])
+        self.channels = int(self.input_shape[-1]) if len(self.input_shape) > 1 else 1
+        self.levels = levels
+        self.train_variance = train_variance
+        self.latent_dim = latent_dim
+        self.num_embeddings = num_embeddings
+        self.down_depth, self.strides = list(down_depth), list(strides)
+        self.cdt = _dtype(dtype)
+        self.device = torch.device(device)
+        self.name = name
+        self.process_group = process_group
+
+        self.vqs = [VectorQuantizer(num_embeddings, latent_dim, level=l, name=f"vector_quantizer_{l}",
+                                    device=self.device, seed=codebook_seed + 1000 * l, reset_seed=reset_seed)
+                    for l in range(levels)]
+        self.encoders = [Encoder(output_dim=latent_dim, residual_width=residual_width, residual_depth=residual_depth,
+                                 depth=l + 1, down_depth=self.down_depth[:l + 1], strides=self.strides[:l + 1],
+                                 dilation_factor=dilation_factor, name=f"encoder_{l}") for l in range(levels)]
+        self.decoders = [Decoder(output_dim=self.channels, embed_width=latent_dim, residual_width=residual_width,
+                                 residual_depth=residual_depth, depth=l + 1, down_depth=self.down_depth[:l + 1],
+                                 strides=self.strides[:l + 1], dilation_factor=dilation_factor, name=f"decoder_{l}")
+                         for l in range(levels)]
+        self.store = ParamStore()
+        for l in range(levels):
+            d = self.encoders[l].build(self.store, f"enc{l}", self.channels, self.cdt)
+            assert d == latent_dim
+            self.decoders[l].build(self.store, f"dec{l}", latent_dim, self.cdt)
+        self.latent_lens = []
+        for l in range(levels):
+            t = self.T
+            for b in range(l + 1):
+                for _ in range(self.down_depth[b]):
+                    t = -(-t // self.strides[b])
+            self.latent_lens.append(t)
+        self.hops = [self.T // t for t in self.latent_lens]  # 8 / 32 / 128 at down_depth [3,2,2] (vqvae.py:54)
+
+        # all-reduce bucket: [grads (P, padded) | per-level VQ stats | per-level (recon, commit, spectral)]
+        P = (self.store.size + 63) // 64 * 64
+        stats = [vq.stats_size() for vq in self.vqs]
+        self._P = P
+        self.bucket = torch.zeros(P + sum(stats) + 3 * levels, dtype=torch.float32, device=self.device)
+        self.store.materialize(self.device, grad_buffer=self.bucket[:P], seed=seed)
+        off = P
+        for vq, n in zip(self.vqs, stats):
+            vq.bind_stats(self.bucket[off:off + n])
+            off += n
+        self._stats_region = self.bucket[P:]
+        self.loss_slots = self.bucket[off:].view(levels, 3)
+        for l, vq in enumerate(self.vqs):
+            vq.commit = self.loss_slots[l, 1:2]
+
+        # metric trackers (vqvae.py:77-89 + VectorQuantizer.py:62-64), one device accumulator
+        names = ["loss", "recon_loss", "vqvae_loss", "spectral_loss"]
+        for l in range(levels):
+            names += [f"[{l}]level_loss", f"[{l}]recon_loss", f"[{l}]vq_loss", f"[{l}]spectral_loss",
+                      f"[{l}]batch_codebook_usage", f"[{l}]codebook_usage", f"[{l}]codebook_entropy"]
+        self.metric_names = names
+        self._macc = torch.zeros(len(names), 2, dtype=torch.float32, device=self.device)
+        self.optimizer: Optional[Adam] = None
+        self.vqvaes = [_LevelModel(self, l) for l in range(levels)]
+        self._graph = None
+
+    # ------------------------------------------------------------------ keras-like API
+    def compile(self, optimizer=None, **kwargs):
+        self.optimizer = optimizer or Adam()
+        self.optimizer.build(self.store)
+
+    @property
+    def metrics(self):
+        return list(self.metric_names)
+
+    def reset_metrics(self):
+        self._macc.zero_()
+        for vq in self.vqs:
+            for m in vq.metrics:
+                m.reset_state()
+
+    def get_quantizer(self):
+        return self.vqs[0]
+
+    def _as_input(self, data) -> torch.Tensor:
+        x = data[0] if isinstance(data, (tuple, list)) else data
+        x = torch.as_tensor(x) if not isinstance(x, torch.Tensor) else x
+        x = x.to(device=self.device, dtype=torch.float32)
+        if x.dim() == 2:
+            x = x.unsqueeze(-1)
+        if tuple(x.shape[1:]) != (self.T, self.channels):
+            raise ValueError(f"input shape {tuple(x.shape)} does not match keras.Input{(self.T, self.channels)}")
+        return x.contiguous()
+
+    def _world(self) -> int:
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.process_group)
+        return 1
+
+    def _rank(self) -> int:
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(self.process_group)
+        return 0
+
+    # ------------------------------------------------------------------ the step
+    def _compute(self, x: torch.Tensor, training_grads: bool):
+        """Forward (+ backward when training_grads) of every level; EMA sums into the bucket."""
+        self._stats_region.zero_()
+        world, rank = self._world(), self._rank()
+        target = SpectralTarget(x)
+        B = x.shape[0]
+        for l in range(self.levels):
+            enc, vq, dec = self.encoders[l], self.vqs[l], self.decoders[l]
+            z = enc.forward(x, save=training_grads)
+            n_loc = z.shape[0] * z.shape[1]
+            q, _ = vq.forward(z, training=True, row_offset=rank * n_loc, n_global=world * n_loc,
+                              save=training_grads)
+            r = dec.forward(q, save=training_grads)
+            spec, dr_spec = multispectral_loss_and_grad(target, r)
+            self.loss_slots[l, 2].copy_(spec)
+            dr = torch.empty_like(r)
+            V.mse_loss(x, r, dr_spec, dr, self.loss_slots[l, 0:1])
+            if training_grads:
+                dq = dec.backward(dr)
+                dz = vq.backward(dq, n_global=n_loc)
+                enc.backward(dz)
+
+    def _update(self, apply_grads: bool):
+        world = self._world()
+        if apply_grads:
+            self.optimizer.apply(self.store, grad_scale=1.0 / world)
+        for vq in self.vqs:
+            vq.apply_ema(update_trackers=False)
+        vals = self.loss_slots * (1.0 / world)
+        lvl = vals.sum(dim=1)
+        tot = torch.cat([lvl.sum().reshape(1), vals.sum(dim=0)])
+        per = torch.cat([lvl.reshape(-1, 1), vals, torch.stack([vq.vq_metrics for vq in self.vqs])], dim=1)
+        self._macc[:, 0] += torch.cat([tot, per.reshape(-1)])
+        self._macc[:, 1] += 1.0
+
+    def _exchange(self):
+        if self._world() > 1:
+            dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM, group=self.process_group)
+
+    def results(self) -> Dict[str, torch.Tensor]:
+        res = self._macc[:, 0] / self._macc[:, 1].clamp(min=1.0)
+        return {n: res[i] for i, n in enumerate(self.metric_names)}
+
+    def train_step(self, data):
+        """vqvae.py:111-146. Returns the running-mean metric dict (0-dim device tensors)."""
+        if self.optimizer is None:
+            self.compile()
+        x = self._as_input(data)
+        if self._graph is not None and x.shape == self._graph_x.shape:
+            self._graph_x.copy_(x)
+            self._replay()
+            return self.results()
+        self._compute(x, training_grads=True)
+        self._exchange()
+        self._update(apply_grads=True)
+        return self.results()
+
+    def test_step(self, data):
+        """vqvae.py:148-172 — forward + losses; the VQ EMA runs (reference default training=True)."""
+        x = self._as_input(data)
+        with torch.no_grad():
+            self._compute(x, training_grads=False)
+            self._exchange()
+            self._update(apply_grads=False)
+        return self.results()
+
+    # ------------------------------------------------------------------ hipGraph capture
+    def capture_train_step(self, x_example, warmup: int = 2):
+        """Run `warmup` eager steps (real steps) then record one full train step as a hipGraph; later
+        train_step calls with this batch shape copy the batch in and replay. With a process group the
+        step is two graphs around the eager RCCL all_reduce."""
+        if self.optimizer is None:
+            self.compile()
+        x = self._as_input(x_example)
+        self._graph_x = x.clone()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._compute(self._graph_x, True)
+                self._exchange()
+                self._update(True)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._graph_pool = torch.cuda.graph_pool_handle()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=self._graph_pool):
+            self._compute(self._graph_x, True)
+            if self._world() == 1:
+                self._update(True)
+        g2 = None
+        if self._world() > 1:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=self._graph_pool):
+                self._update(True)
+        self._graph = (g1, g2)
+        torch.cuda.synchronize(self.device)
+
+    def _replay(self):
+        g1, g2 = self._graph
+        g1.replay()
+        if g2 is not None:
+            self._exchange()
+            g2.replay()
+
+    # ------------------------------------------------------------------ inference API
+    def _level_forward_only(self, x, l, training):
+        with torch.no_grad():
+            z = self.encoders[l].forward(x)
+            if training:
+                self.vqs[l].stats.zero_()
+            q, _ = self.vqs[l].forward(z, training=training)
+            if training:
+                self.vqs[l].apply_ema()
+            return self.decoders[l].forward(q)
+
+    def __call__(self, x, training=False):
+        """vqvae.py:178-206 -> (recons, {level_losses, recon_losses, commit_losses, spec_losses})."""
+        if isinstance(x, tuple):
+            x = x[0]
+        x = self._as_input(x)
+        target = SpectralTarget(x)
+        recons, out = [], {"level_losses": [], "recon_losses": [], "commit_losses": [], "spec_losses": []}
+        with torch.no_grad():
+            for l in range(self.levels):
+                r = self._level_forward_only(x, l, training)
+                recons.append(r)
+                spec, _ = multispectral_loss_and_grad(target, r)
+                recon = ((x - r) ** 2).mean()
+                commit = self.vqs[l].commit[0].clone()
+                out["level_losses"].append(recon + commit + spec)
+                out["recon_losses"].append(recon)
+                out["commit_losses"].append(commit)
+                out["spec_losses"].append(spec)
+        return recons, out
+
+    call = __call__
+
+    def encode_level(self, x, level, chunk=1):
+        """vqvae.py:208-219 -> (B, T_l) int64 codes."""
+        x = self._as_input(x)
+        with torch.no_grad():
+            z = self.encoders[level].forward(x)
+            idx = self.vqs[level].get_code_indices(z.reshape(-1, self.latent_dim))
+        return idx.view(z.shape[0], z.shape[1])
+
+    def encode(self, x, start_level=0, end_level=None):
+        end_level = self.levels if end_level is None else end_level
+        return [self.encode_level(x, l) for l in range(start_level, end_level)]
+
+    def decode_level(self, zq, level, chunk=1):
+        """vqvae.py:238-251: one_hot(zq) @ E^T (a row gather of ET) -> decoder."""
+        zq = torch.as_tensor(zq, device=self.device).long()
+        with torch.no_grad():
+            q = self.vqs[level].ET[zq.reshape(-1)].view(*zq.shape, self.latent_dim).to(self.cdt).contiguous()
+            return self.decoders[level].forward(q)
+
+    def decode(self, zq, level=0):
+        return self.decode_level(zq, level)
+
+    # ------------------------------------------------------------------ training loop / state
+    def fit(self, x=None, y=None, batch_size=32, epochs=1, shuffle=True, seed=0, verbose=0):
+        """Minimal keras fit: metrics reset per epoch; returns history of epoch-end results."""
+        if self.optimizer is None:
+            self.compile()
+        xs = np.asarray(x, np.float32)
+        n = xs.shape[0]
+        rng = np.random.default_rng(seed)
+        hist = []
+        for ep in range(epochs):
+            self.reset_metrics()
+            order = rng.permutation(n) if shuffle else np.arange(n)
+            for i in range(0, n - batch_size + 1, batch_size):
+                self.train_step(xs[order[i:i + batch_size]])
+            res = {k: float(v) for k, v in self.results().items()}
+            hist.append(res)
+            if verbose:
+                print(f"epoch {ep + 1}/{epochs}", res)
+        return hist
+
+    def get_weights(self) -> Dict[str, np.ndarray]:
+        return self.store.values()
+
+    def set_weights(self, vals: Dict[str, np.ndarray]):
+        self.store.set_values(vals)
+
+    def get_vq_state(self):
+        return [vq.get_state() for vq in self.vqs]
+
+    def set_vq_state(self, states):
+        for vq, st in zip(self.vqs, states):
+            vq.set_state(st)
+
+    @property
+    def trainable_variables(self):
+        return list(chain.from_iterable(m.trainable_variables for m in self.vqvaes))
+
+    def state_dict(self):
+        """Checkpoint payload: weights, Adam moments and step, VQ state."""
+        sd = {"weights": self.store.flat.detach().cpu().clone(), "vq": self.get_vq_state()}
+        if self.optimizer is not None and self.optimizer.m is not None:
+            sd.update({"adam_m": self.optimizer.m.cpu().clone(), "adam_v": self.optimizer.v.cpu().clone(),
+                       "iterations": int(self.optimizer.iterations.item())})
+        return sd
+
+    def load_state_dict(self, sd):
+        self.store.flat.copy_(sd["weights"].to(self.device))
+        self.set_vq_state(sd["vq"])
+        if "adam_m" in sd:
+            if self.optimizer is None:
+                self.compile()
+            self.optimizer.m.copy_(sd["adam_m"].to(self.device))
+            self.optimizer.v.copy_(sd["adam_v"].to(self.device))
+            self.optimizer.iterations.fill_(int(sd["iterations"]))
