@@ -346,15 +346,16 @@ class RefVQVAE:
 
     @staticmethod
     def _scalars(total, infos):
-        out = {"loss": float(total.detach())}
-        out["recon_loss"] = float(sum(float(i["recon_loss"]) for i in infos))
-        out["vqvae_loss"] = float(sum(float(i["commit"]) for i in infos))
-        out["spectral_loss"] = float(sum(float(i["spectral_loss"]) for i in infos))
+        f = lambda v: float(v.detach()) if isinstance(v, torch.Tensor) else float(v)  # noqa: E731
+        out = {"loss": f(total)}
+        out["recon_loss"] = sum(f(i["recon_loss"]) for i in infos)
+        out["vqvae_loss"] = sum(f(i["commit"]) for i in infos)
+        out["spectral_loss"] = sum(f(i["spectral_loss"]) for i in infos)
         for l, i in enumerate(infos):
-            out[f"[{l}]level_loss"] = float(i["level_loss"])
-            out[f"[{l}]recon_loss"] = float(i["recon_loss"])
-            out[f"[{l}]vq_loss"] = float(i["commit"])
-            out[f"[{l}]spectral_loss"] = float(i["spectral_loss"])
+            out[f"[{l}]level_loss"] = f(i["level_loss"])
+            out[f"[{l}]recon_loss"] = f(i["recon_loss"])
+            out[f"[{l}]vq_loss"] = f(i["commit"])
+            out[f"[{l}]spectral_loss"] = f(i["spectral_loss"])
             for k in ("batch_usage", "usage", "entropy"):
                 if k in i:
                     key = {"batch_usage": "batch_codebook_usage", "usage": "codebook_usage",

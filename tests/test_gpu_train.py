@@ -1,15 +1,16 @@
 """End-to-end VQVAE.train_step parity (vqvae.py:111-146) vs the CPU oracle (fp64), plus the reference's
 other entry points (test_step, call, encode, decode) and hipGraph replay.
 
-fp32 model: per-level losses rel <= 1e-5; gradients: median over tensors of the max-norm relative error
-<= 1e-5, and every tensor's relative L2 error against the fp64 oracle <= max(4 x the oracle's OWN fp32
-error, 2e-4). A fixed per-tensor bound is not usable: a pre-activation within fp32 noise of 0 takes the
-other ReLU branch in fp64, and a bias gradient (a sum with cancellation) amplifies that one term — the
-reference trains in fp32, so fp32 against fp64 is the yardstick (measured: zero index mismatches, median
-error 7e-7, a few conv_a tensors up to 2.5e-3 max-norm); weights and
-codebooks after two Adam/EMA steps <= 1e-4 (L2); usage counts N_t equal on >= 99 % of codes (a code can
-move only when a row sits on a near-tie). bf16 model: losses rel <= 3e-2, gradient
-relative L2 <= 0.15 per tensor.
+fp32 model, end to end against the fp64 oracle: per-level losses rel <= 1e-5; the median over tensors of
+the max-norm gradient error <= 1e-5; every tensor's relative L2 gradient error <= 5e-3. The per-tensor
+bound has to be loose: a pre-activation within fp32 rounding of 0 takes the other ReLU branch in fp64,
+and that one element propagates to every earlier layer (measured on cfg1: one such element in
+enc0/blk0/res2/rb1 gives 2.7e-3 there while every other block is at 1e-7). The strict check is
+test_resblock_backward_teacher_forced: each GPU residual block's backward against fp64 autograd of the
+same block on the GPU's own saved input with the GPU's ReLU masks — no branch can flip, bound 1e-6.
+Weights and codebooks after two Adam/EMA steps: relative L2 <= 1e-3; usage counts N_t equal on >= 99 %
+of codes (a code can move only when a row sits on a near-tie). bf16 model: losses rel
+<= 3e-2, gradient relative L2 <= 0.15 per tensor.
 """
 import numpy as np
 import pytest
@@ -52,12 +53,11 @@ def _l2(a, b):
     return float(np.linalg.norm((np.asarray(a, np.float64) - b).ravel()) / max(np.linalg.norm(np.ravel(b)), 1e-30))
 
 
-def _check_grads(grads, ref_grads, l2_tol, med_tol, tag, yardstick=None):
+def _check_grads(grads, ref_grads, l2_tol, med_tol, tag):
     maxrel = {n: _rel(grads[n], g.numpy()) for n, g in ref_grads.items()}
     l2 = {n: _l2(grads[n], g.numpy()) for n, g in ref_grads.items()}
     for n in l2:
-        tol = l2_tol if yardstick is None else max(l2_tol, 4 * _l2(yardstick[n].numpy(), ref_grads[n].numpy()))
-        assert l2[n] < tol, f"{tag}: grad {n} relative L2 {l2[n]:.3e} (allowed {tol:.3e})"
+        assert l2[n] < l2_tol, f"{tag}: grad {n} relative L2 {l2[n]:.3e}"
     med = float(np.median(list(maxrel.values())))
     assert med < med_tol, f"{tag}: median max-norm grad error {med:.3e}"
 
@@ -68,14 +68,12 @@ def test_train_step_fp32_matches_oracle(cuda, name):
     cfg, B = c["cfg"], c["B"]
     params, vq = R.init_params(cfg, 1), R.init_vq_state(cfg, 2)
     ref = R.RefVQVAE(cfg, params, vq, dtype=torch.float64)
-    ref32 = R.RefVQVAE(cfg, params, vq, dtype=torch.float32)   # yardstick: the oracle's own fp32 error
     m = _model(cfg, B, "fp32", params, vq)
     x0 = R.synthetic_batch(B, cfg.input_len, seed=11)
     x1 = R.synthetic_batch(B, cfg.input_len, seed=12)
     hist = []
     for step, x in enumerate((x0, x1)):
         out = ref.train_step(x)
-        ref32.train_step(x)
         hist.append(out)
         res = {k: float(v) for k, v in m.train_step(x).items()}
         torch.cuda.synchronize()
@@ -83,18 +81,18 @@ def test_train_step_fp32_matches_oracle(cuda, name):
             want = float(np.mean([h[k] for h in hist]))
             tol = 1e-5 if "usage" not in k and "entropy" not in k else 2e-2
             assert abs(res[k] - want) <= tol * max(abs(want), 1e-3), f"step {step} {k}: gpu {res[k]} oracle {want}"
-        _check_grads(m.store.grads(), ref.last["grads"], 2e-4, 1e-5, f"step {step}", ref32.last["grads"])
+        _check_grads(m.store.grads(), ref.last["grads"], 5e-3, 1e-5, f"step {step}")
     w = m.get_weights()
     ow, ovq = ref.state_numpy()
     for n in ow:
-        assert _l2(w[n], ow[n]) < 1e-4, f"weight {n}"
+        assert _l2(w[n], ow[n]) < 1e-3, f"weight {n}"
     for l, st in enumerate(m.get_vq_state()):
         o = ovq[l]
         same = np.isclose(st["N_t"], o["N_t"], rtol=1e-6, atol=1e-6)
         assert same.mean() >= 0.99, f"level {l}: N_t differs on {(~same).sum()} codes"
         good = np.where(same)[0]
-        assert _rel(st["m_t"][:, good], o["m_t"][:, good]) < 1e-4
-        assert _rel(st["embeddings"][:, good], o["embeddings"][:, good]) < 1e-4
+        assert _l2(st["m_t"][:, good], o["m_t"][:, good]) < 1e-3
+        assert _l2(st["embeddings"][:, good], o["embeddings"][:, good]) < 1e-3
         assert st["calls"] == o["calls"] == 2
 
 
@@ -183,3 +181,88 @@ def test_state_dict_roundtrip_resume(cuda):
     wa, wb = a.get_weights(), b.get_weights()
     for n in wa:
         assert _rel(wb[n], wa[n]) < 5e-4, n  # fp32 atomics order in the EMA sums differs run to run
+
+
+@pytest.mark.parametrize("name", ["cfg1", "tiny"])
+def test_resblock_backward_teacher_forced(cuda, name):
+    """Every residual block's backward (resnet.py:7-29) on the GPU vs fp64 autograd of the same block,
+    fed the GPU's own saved input and upstream gradient, with ReLU masks taken from the GPU activations."""
+    import torch.nn.functional as F
+    import resnet
+    c = CONFIGS[name]
+    cfg, B = c["cfg"], c["B"]
+    params, vq = R.init_params(cfg, 1), R.init_vq_state(cfg, 2)
+    m = _model(cfg, B, "fp32", params, vq)
+    log = []
+    orig = resnet.ResnetConv1DBlock.backward
+
+    def spy(self, dy):
+        xs, h = self._saved
+        rec = dict(blk=self, x=xs.double().cpu(), h=h.double().cpu(), dy=dy.double().cpu())
+        dx = orig(self, dy)
+        rec["dx"] = dx.double().cpu()
+        log.append(rec)
+        return dx
+
+    resnet.ResnetConv1DBlock.backward = spy
+    try:
+        m.train_step(R.synthetic_batch(B, cfg.input_len, seed=11))
+    finally:
+        resnet.ResnetConv1DBlock.backward = orig
+    g = m.store.grads()
+    assert len(log) == sum(1 for n in g if n.endswith("conv_a/kernel"))
+    for rec in log:
+        blk = rec["blk"]
+        na, nb = blk.conv_a.name, blk.conv_b.name
+        W = {k: torch.tensor(params[k], dtype=torch.float64, requires_grad=True)
+             for k in (f"{na}/kernel", f"{na}/bias", f"{nb}/kernel", f"{nb}/bias")}
+        xv = rec["x"].clone().requires_grad_(True)
+        h = R.conv1d(xv * (rec["x"] > 0), W[f"{na}/kernel"], W[f"{na}/bias"], 1, blk.dilation)
+        assert _l2(rec["h"].numpy(), h.detach().numpy()) < 1e-6, f"{na}: forward h"
+        y = xv + R.conv1d(h * (rec["h"] > 0), W[f"{nb}/kernel"], W[f"{nb}/bias"], 1, 1)
+        grads = torch.autograd.grad((y * rec["dy"]).sum(), [xv] + list(W.values()))
+        assert _l2(rec["dx"].numpy(), grads[0].numpy()) < 1e-6, f"{na}: dx"
+        for (k, _), gr in zip(W.items(), grads[1:]):
+            assert _l2(g[k], gr.numpy()) < 1e-6, f"{k}"
+
+
+def test_product_against_golden_micro(cuda):
+    """libvqa fp32 train steps vs the committed oracle fixture tests/golden/micro.npz (width 8, latent 4,
+    K=64: the thin / generic kernel paths)."""
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(gold, "micro.npz"))
+    meta = json.load(open(os.path.join(gold, "micro.json")))
+    cfg = R.RefConfig(**meta["config"])
+    params = {k[5:]: z[k] for k in z.files if k.startswith("init/")}
+    vq = [{"embeddings": z[f"vq_init{l}/embeddings"], "m_t": z[f"vq_init{l}/embeddings"],
+           "N_t": np.ones(cfg.num_embeddings, np.float32), "calls": 0} for l in range(cfg.levels)]
+    m = _model(cfg, meta["batch"], "fp32", params, vq)
+    for s in range(meta["steps"]):
+        res = {k: float(v) for k, v in m.train_step(z[f"x{s}"]).items()}
+        want = {k: float(np.mean([meta["metrics"][i][k] for i in range(s + 1)])) for k in res}
+        for k in res:
+            tol = 1e-5 if "usage" not in k and "entropy" not in k else 2e-2
+            assert abs(res[k] - want[k]) <= tol * max(abs(want[k]), 1e-3), (s, k, res[k], want[k])
+        g = m.store.grads()
+        meds = [_rel(g[n[len(f"grad{s}/"):]], z[n]) for n in z.files if n.startswith(f"grad{s}/")]
+        assert np.median(meds) < 1e-5
+    w = m.get_weights()
+    for n in params:
+        assert _l2(w[n], z[f"final/{n}"]) < 1e-3, n
+
+
+def test_product_against_golden_cfg1_scalars(cuda):
+    import json
+    import os
+    meta = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg1.json")))
+    cfg = R.RefConfig(**meta["config"])
+    m = _model(cfg, meta["batch"], "fp32", R.init_params(cfg, 1), R.init_vq_state(cfg, 2))
+    res = {k: float(v) for k, v in m.train_step(R.synthetic_batch(meta["batch"], cfg.input_len,
+                                                                   seed=meta["x_seeds"][0])).items()}
+    for k in ("loss", "recon_loss", "vqvae_loss", "spectral_loss", "[0]batch_codebook_usage"):
+        assert abs(res[k] - meta["metrics"][0][k]) <= 1e-5 * max(abs(meta["metrics"][0][k]), 1e-3), k
+    g = m.store.grads()
+    rel = [abs(np.linalg.norm(g[n]) - v) / v for n, v in meta["grad_norms"][0].items()]
+    assert np.median(rel) < 1e-5 and max(rel) < 5e-3

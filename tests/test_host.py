@@ -1,0 +1,93 @@
+"""Host-side logic, no GPU: the product's layer structure / parameter registration / init vs the oracle,
+the DP bucket layout, dilation schedules, and the loud failure modes of the C-ABI binding."""
+import numpy as np
+import pytest
+import torch
+
+import vqa_dp
+import vqa_lib as V
+from encdec import Decoder, Encoder
+from oracle import vqvae_ref as R
+from resnet import DilatedResnet1D
+from vqa_layers import ParamStore
+
+CFG2 = R.RefConfig(input_len=65536, levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2],
+                   num_embeddings=2048, residual_width=32, residual_depth=4, dilation_factor=3)
+TINY = R.RefConfig(input_len=2048, levels=2, latent_dim=8, down_depth=[2, 1], strides=[2, 2], num_embeddings=1024,
+                   residual_width=32, residual_depth=2, dilation_factor=3)
+
+
+def _product_store(cfg):
+    store = ParamStore()
+    for l in range(cfg.levels):
+        enc = Encoder(cfg.latent_dim, cfg.residual_width, cfg.residual_depth, l + 1, cfg.down_depth[:l + 1],
+                      cfg.strides[:l + 1], cfg.dilation_factor)
+        dec = Decoder(1, cfg.latent_dim, cfg.residual_width, cfg.residual_depth, l + 1, cfg.down_depth[:l + 1],
+                      cfg.strides[:l + 1], cfg.dilation_factor)
+        assert enc.build(store, f"enc{l}", 1, torch.bfloat16) == cfg.latent_dim
+        assert dec.build(store, f"dec{l}", cfg.latent_dim, torch.bfloat16) == 1
+    return store
+
+
+@pytest.mark.parametrize("cfg", [CFG2, TINY])
+def test_parameter_structure_matches_oracle(cfg):
+    store = _product_store(cfg)
+    assert [(n, s) for n, s, _ in store.specs] == R.param_specs(cfg)
+
+
+def test_cfg2_parameter_count():
+    """968,835 trainable parameters in 570 tensors at cfg2."""
+    store = _product_store(CFG2)
+    assert store.size == 968835 and len(store.specs) == 570
+
+
+def test_init_matches_oracle_bitwise():
+    store = _product_store(TINY)
+    want = R.init_params(TINY, 1)
+    got = store.init_values(1)
+    assert got.keys() == want.keys()
+    for n in want:
+        assert np.array_equal(got[n], want[n]), n
+
+
+@pytest.mark.parametrize("depth,f,rev,cycle,want", [(4, 3, False, None, [1, 3, 9, 27]), (4, 3, True, None, [27, 9, 3, 1]),
+                                                    (8, 3, False, 4, [1, 3, 9, 27, 1, 3, 9, 27]), (3, 1, False, None, [1, 1, 1])])
+def test_dilation_schedule(depth, f, rev, cycle, want):
+    """resnet.py:44-55."""
+    assert DilatedResnet1D(32, depth, f, rev, cycle).dilations == want
+
+
+def test_bucket_layout_cfg2():
+    stats = [2 * 2048 * 64 + 2048] * 3
+    lay = vqa_dp.bucket_layout(968835, stats, 3)
+    P0, P1 = lay["grads"]
+    assert P0 == 0 and P1 >= 968835 and P1 % 64 == 0
+    prev = P1
+    for a, b in lay["stats"]:
+        assert a == prev and b - a == stats[0]
+        prev = b
+    assert lay["losses"] == (prev, prev + 9) and lay["total"] == prev + 9
+    mb = lay["total"] * 4 / 1e6
+    # 7.0 MB per step on the wire at cfg2: 3.9 MB grads + 3 x (m_sum 0.5 MB + n_sum + reset rows 0.5 MB)
+    assert 6.5 < mb < 7.5, mb
+    sl = vqa_dp.vq_stats_slices(2048, 64)
+    assert sl["m_sumT"] == (0, 131072) and sl["n_sum"] == (131072, 133120) and sl["RT"][1] == stats[0]
+
+
+def test_single_rank_dp_helpers():
+    assert vqa_dp.world_size() == 1 and vqa_dp.rank() == 0
+    assert vqa_dp.global_row_range(1000) == (0, 1000)
+    b = torch.ones(10)
+    assert vqa_dp.exchange(b) == 1 and float(b.sum()) == 10
+
+
+def test_binding_rejects_host_tensors():
+    with pytest.raises(V.VQAError, match="device tensors"):
+        V.ptr(torch.zeros(4))
+
+
+def test_binding_fails_loudly_without_library(monkeypatch):
+    monkeypatch.setattr(V, "LIB_PATH", "/nonexistent/libvqa.so")
+    monkeypatch.setattr(V, "_lib", None)
+    with pytest.raises(ImportError, match="no CPU fallback"):
+        V.lib()

@@ -98,6 +98,88 @@ __global__ __launch_bounds__(256) void gather_direct_kernel(GatherArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Thin gather conv for the 1-channel waveform layers (C <= 8 or O <= 8): weights in LDS (fp32), each
+// thread owns OV consecutive output channels of one row; 16-byte loads along C when C % 8 == 0.
+template <class T> __device__ __forceinline__ void ld8_(const T* p, float* v);
+template <> __device__ __forceinline__ void ld8_<bf16>(const bf16* p, float* v) {
+  const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <> __device__ __forceinline__ void ld8_<float>(const float* p, float* v) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = a[j];
+    v[j + 4] = b[j];
+  }
+}
+
+template <class TX, class TY, int OV>
+__global__ __launch_bounds__(256) void gather_thin_kernel(GatherArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* wl = (float*)smem;  // [K][C][O]
+  const int KCO = a.K * a.C * a.O;
+  for (int e = threadIdx.x; e < KCO; e += blockDim.x) {
+    const int o = e % a.O, c = (e / a.O) % a.C, k = e / (a.O * a.C);
+    wl[e] = weff(a, k, c, o);
+  }
+  __syncthreads();
+  const TX* X = (const TX*)a.x;
+  const int OG = a.O / OV;
+  const long long total = (long long)a.B * a.T_out * OG;
+  const bool relu = a.flags & VQA_PRE_RELU;
+  const bool vec = (a.C % 8) == 0;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int og = (int)(e % OG);
+    const long long r = e / OG;
+    const int t = (int)(r % a.T_out);
+    const int n = (int)(r / a.T_out);
+    float acc[OV];
+#pragma unroll
+    for (int q = 0; q < OV; ++q) acc[q] = 0.f;
+    for (int k = 0; k < a.K; ++k) {
+      const int ti = t * a.S + k * a.D - a.P;
+      if (ti < 0 || ti >= a.T_in) continue;
+      const TX* xr = X + ((long long)n * a.T_in + ti) * a.C;
+      const float* wk = wl + (size_t)k * a.C * a.O + og * OV;
+      if (vec) {
+        for (int c0 = 0; c0 < a.C; c0 += 8) {
+          float xv[8];
+          ld8_(xr + c0, xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xj = relu ? fmaxf(xv[j], 0.f) : xv[j];
+#pragma unroll
+            for (int q = 0; q < OV; ++q) acc[q] += xj * wk[(c0 + j) * a.O + q];
+          }
+        }
+      } else {
+        for (int c = 0; c < a.C; ++c) {
+          float xs = ld(xr + c);
+          if (relu) xs = fmaxf(xs, 0.f);
+#pragma unroll
+          for (int q = 0; q < OV; ++q) acc[q] += xs * wk[c * a.O + q];
+        }
+      }
+    }
+    const int o0 = og * OV;
+    const long long oi = out_index(a, n, t, o0);
+    if (oi < 0) continue;
+    const int bo = bias_index(a, o0);
+#pragma unroll
+    for (int q = 0; q < OV; ++q) {
+      float v = acc[q];
+      if (a.bias) v = v + a.bias[bo + q];
+      if (a.flags & VQA_POST_MASK) v = ld((const TY*)a.mask + oi + q) > 0.f ? v : 0.f;
+      if (a.flags & VQA_ADD_RESIDUAL) v = ld((const TY*)a.resid + oi + q) + v;
+      st((TY*)a.y + oi + q, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // MFMA fragment traits. bf16: v_mfma_f32_16x16x32_bf16 (8 consecutive channels per lane, one
 // 16-byte LDS read). fp32: v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain; used for parity runs).
 template <class T> struct Mfma;
@@ -252,8 +334,13 @@ struct WgradArgs {
   float* ws;
   int B, T_in, T_out, C, O, K, S, D, P;
   int CH, nchunk;
-  int flags;
+  int flags;  // VQA_PRE_RELU, VQA_X_F32, VQA_Y_F32, WG_DB_FROM_X
+  int nb;     // bias entries per partial: O (bias = column sums of g) or C (WG_DB_FROM_X)
 };
+
+// bias gradient = column sums of the INPUT x over the rows this workgroup owns (conv-transpose bias:
+// its output-gradient is the gather input of the weight gradient)
+constexpr int WG_DB_FROM_X = 1 << 8;
 
 template <class T, int C, int O, int TT>
 __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
@@ -279,8 +366,9 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
 #pragma unroll
   for (int i = 0; i < MAXTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
-  const int dbo = threadIdx.x % O, dbr = threadIdx.x / O;
-  constexpr int DBSTEP = 256 / O;
+  const bool db_x = a.flags & WG_DB_FROM_X;
+  const int NB = db_x ? C : O;
+  const int dbo = threadIdx.x % NB, dbr = threadIdx.x / NB, dbstep = 256 / NB;
 
   for (int t0 = tbeg; t0 < tend; t0 += TT) {
     const int nrows = min(TT, tend - t0);
@@ -288,7 +376,11 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
     stage_rows<T, C>(xl, XS, (const T*)a.x + (long long)n * a.T_in * C, 0, a.T_in, t0 * a.S - a.P, rows_in,
                      a.flags & VQA_PRE_RELU);
     __syncthreads();
-    for (int r = dbr; r < nrows; r += DBSTEP) dbacc += (float)gl[r * GS + dbo];
+    if (db_x) {
+      for (int r = a.P + dbr; r < a.P + nrows * a.S; r += dbstep) dbacc += (float)xl[r * XS + dbo];
+    } else {
+      for (int r = dbr; r < nrows; r += dbstep) dbacc += (float)gl[r * GS + dbo];
+    }
 #pragma unroll
     for (int ti = 0; ti < MAXTW; ++ti) {
       const int tile = wave + 4 * ti;
@@ -308,7 +400,7 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
     __syncthreads();
   }
 
-  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(a.K * C * O + O);
+  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(a.K * C * O + NB);
 #pragma unroll
   for (int ti = 0; ti < MAXTW; ++ti) {
     const int tile = wave + 4 * ti;
@@ -324,10 +416,146 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
   }
   red[threadIdx.x] = dbacc;
   __syncthreads();
-  if (threadIdx.x < O) {
+  if (threadIdx.x < NB) {
     float s = 0.f;
-    for (int r = 0; r < DBSTEP; ++r) s += red[r * O + threadIdx.x];
+    for (int r = 0; r < dbstep; ++r) s += red[r * NB + threadIdx.x];
     out[a.K * C * O + threadIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Thin weight gradients for the 1-channel waveform layers. Threads = RL row lanes x VL lanes of 8
+// consecutive channels along the WIDE side; 16-byte loads along it; LDS reduction over row lanes.
+//   WIDE_X: C % 8 == 0, O <= 2 (decoder output conv, C=64 -> O=1)
+//   WIDE_G: O % 8 == 0, C <= 2 (first encoder conv, C=1 -> O=32)
+template <class T> __device__ __forceinline__ void ld8(const T* p, float* v);
+template <> __device__ __forceinline__ void ld8<bf16>(const bf16* p, float* v) {
+  const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <> __device__ __forceinline__ void ld8<float>(const float* p, float* v) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = a[j];
+    v[j + 4] = b[j];
+  }
+}
+template <class T> __device__ __forceinline__ void st8(T* p, const float* v);
+template <> __device__ __forceinline__ void st8<bf16>(bf16* p, const float* v) {
+  bf16x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
+  *(bf16x8*)p = x;
+}
+template <> __device__ __forceinline__ void st8<float>(float* p, const float* v) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+template <class TX, class TG, bool WIDE_X>
+__global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
+  constexpr int KM = 4, NM = 2;  // max taps, max narrow width
+  const int W = WIDE_X ? a.C : a.O;
+  const int NN = WIDE_X ? a.O : a.C;
+  const int VL = W / 8, RL = 256 / VL;
+  const int v = threadIdx.x % VL, rl = threadIdx.x / VL;
+  const int n = blockIdx.y, ch = blockIdx.x;
+  const int tbeg = ch * a.CH, tend = min(a.T_out, tbeg + a.CH);
+  const bool relu = a.flags & VQA_PRE_RELU;
+  const TX* X = (const TX*)a.x + (long long)n * a.T_in * a.C;
+  const TG* G = (const TG*)a.g + (long long)n * a.T_out * a.O;
+  float acc[KM][NM][8];
+  float bacc[8];
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+#pragma unroll
+    for (int i = 0; i < NM; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][i][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  if (rl < RL) {
+    for (int t = tbeg + rl; t < tend; t += RL) {
+      if (WIDE_X) {
+        float gv[NM];
+#pragma unroll
+        for (int i = 0; i < NM; ++i) gv[i] = i < NN ? ld(G + (long long)t * a.O + i) : 0.f;
+        if (v == 0)
+#pragma unroll
+          for (int i = 0; i < NM; ++i) bacc[i] += gv[i];
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          const int ti = t * a.S + k * a.D - a.P;
+          if (k < a.K && ti >= 0 && ti < a.T_in) {
+            float xv[8];
+            ld8(X + (long long)ti * a.C + v * 8, xv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              if (relu) xv[j] = fmaxf(xv[j], 0.f);
+#pragma unroll
+              for (int i = 0; i < NM; ++i) acc[k][i][j] += xv[j] * gv[i];
+            }
+          }
+        }
+      } else {
+        float gv[8];
+        ld8(G + (long long)t * a.O + v * 8, gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bacc[j] += gv[j];
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          const int ti = t * a.S + k * a.D - a.P;
+          if (k < a.K && ti >= 0 && ti < a.T_in) {
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+              if (i < NN) {
+                float xs = ld(X + (long long)ti * a.C + i);
+                if (relu) xs = fmaxf(xs, 0.f);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[k][i][j] += xs * gv[j];
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  // reduce over row lanes: per thread KM*NM*8 + 8 values
+  constexpr int PER = KM * NM * 8 + 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = (float*)smem;  // [256][PER]
+  {
+    float* r = red + threadIdx.x * PER;
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+#pragma unroll
+      for (int i = 0; i < NM; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[q++] = acc[k][i][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[q++] = bacc[j];
+  }
+  __syncthreads();
+  const int KCO = a.K * a.C * a.O;
+  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(KCO + a.nb);
+  for (int e = threadIdx.x; e < KCO + a.nb; e += 256) {
+    int vv, q;
+    if (e < KCO) {
+      const int o = e % a.O, c = (e / a.O) % a.C, k = e / (a.O * a.C);
+      const int wide = WIDE_X ? c : o, narrow = WIDE_X ? o : c;
+      vv = wide / 8;
+      q = (k * NM + narrow) * 8 + (wide % 8);
+    } else {
+      const int o = e - KCO;
+      vv = WIDE_X ? 0 : o / 8;
+      q = KM * NM * 8 + (WIDE_X ? o : o % 8);
+    }
+    float sum = 0.f;
+    for (int r = 0; r < RL; ++r) sum += red[(r * VL + vv) * PER + q];
+    out[e] = sum;
   }
 }
 
@@ -360,8 +588,12 @@ __global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
       xl[e] = relu ? fmaxf(v, 0.f) : v;
     }
     __syncthreads();
-    if (threadIdx.x < a.O)
+    if (a.flags & WG_DB_FROM_X) {
+      if (threadIdx.x < a.C)
+        for (int r = a.P; r < a.P + nrows * a.S; ++r) dbacc += xl[r * a.C + threadIdx.x];
+    } else if (threadIdx.x < a.O) {
       for (int r = 0; r < nrows; ++r) dbacc += gl[r * a.O + threadIdx.x];
+    }
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       const int e = threadIdx.x + i * 256;
@@ -374,45 +606,43 @@ __global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
     }
     __syncthreads();
   }
-  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(E + a.O);
+  float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(E + a.nb);
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = threadIdx.x + i * 256;
     if (e < E) out[e] = acc[i];
   }
-  if (threadIdx.x < a.O) out[E + threadIdx.x] = dbacc;
+  if (threadIdx.x < a.nb) out[E + threadIdx.x] = dbacc;
 }
 
-// out1[e] = sum_p ws[p*E + e] for e < E1; out2[e - E1] likewise for e >= E1 (fixed order).
+// out1[e] = sum_p ws[p*E + e] for e < E1, out2[e - E1] likewise for e >= E1. Block = 64 elements x 4
+// part groups; each thread keeps 4 independent partial sums (memory-level parallelism); the groups are
+// combined in a fixed order, so the result is deterministic.
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, int nparts, int E, int E1,
                                                              float* out1, float* out2) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += ws[(size_t)p * E + e];
-  if (e < E1) {
-    if (out1) out1[e] = s;
-  } else if (out2) {
-    out2[e - E1] = s;
+  __shared__ float red[4][64];
+  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (e < E) {
+    int p = grp;
+    for (; p + 12 < nparts; p += 16) {
+      s0 += ws[(size_t)p * E + e];
+      s1 += ws[(size_t)(p + 4) * E + e];
+      s2 += ws[(size_t)(p + 8) * E + e];
+      s3 += ws[(size_t)(p + 12) * E + e];
+    }
+    for (; p < nparts; p += 4) s0 += ws[(size_t)p * E + e];
   }
-}
-
-// column sums of a (rows, O) tensor: partial per workgroup -> ws[wg][O]
-template <class T>
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* y, long long rows, int O, int rows_per_wg,
-                                                            float* ws) {
-  __shared__ float red[256];
-  const long long r0 = (long long)blockIdx.x * rows_per_wg;
-  const long long r1 = min(rows, r0 + rows_per_wg);
-  const int o = threadIdx.x % O, rs = threadIdx.x / O, step = 256 / O;
-  float s = 0.f;
-  for (long long r = r0 + rs; r < r1; r += step) s += ld(y + r * O + o);
-  red[threadIdx.x] = s;
+  red[grp][el] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (threadIdx.x < O) {
-    float t = 0.f;
-    for (int i = 0; i < step; ++i) t += red[i * O + threadIdx.x];
-    ws[(size_t)blockIdx.x * O + threadIdx.x] = t;
+  if (grp == 0 && e < E) {
+    const float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+    if (e < E1) {
+      if (out1) out1[e] = s;
+    } else if (out2) {
+      out2[e - E1] = s;
+    }
   }
 }
 
@@ -498,6 +728,22 @@ static int launch_gather_direct(const GatherArgs& a, hipStream_t s) {
   return VQA_OK;
 }
 
+template <class TX, class TY>
+static int launch_gather_thin(const GatherArgs& a, hipStream_t s) {
+  const int OV = (a.O % 8 == 0) ? 8 : 1;
+  const long long total = (long long)a.B * a.T_out * (a.O / OV);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  const size_t lds = (size_t)a.K * a.C * a.O * sizeof(float);
+  if (OV == 8)
+    hipLaunchKernelGGL((gather_thin_kernel<TX, TY, 8>), dim3((unsigned)blocks), dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((gather_thin_kernel<TX, TY, 1>), dim3((unsigned)blocks), dim3(256), lds, s, a);
+  VQA_LAUNCHED("gather_thin_kernel");
+  return VQA_OK;
+}
+
 int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
   VQA_ARG(a.x && a.w && a.y, "null tensor pointer");
@@ -508,6 +754,13 @@ int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
   if (mfma_ok(a)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
   const bool xf = dtype == VQA_F32 || (a.flags & VQA_X_F32);
   const bool yf = dtype == VQA_F32 || (a.flags & VQA_Y_F32);
+  if ((a.C <= 8 || a.O <= 8) && (size_t)a.K * a.C * a.O * 4 <= 64 * 1024 &&
+      (a.wmode != W_PAIR || (a.O / 2) % 8 == 0 || a.O % 8 != 0)) {
+    if (xf && yf) return launch_gather_thin<float, float>(a, s);
+    if (xf) return launch_gather_thin<float, bf16>(a, s);
+    if (yf) return launch_gather_thin<bf16, float>(a, s);
+    return launch_gather_thin<bf16, bf16>(a, s);
+  }
   if (xf && yf) return launch_gather_direct<float, float>(a, s);
   if (xf) return launch_gather_direct<float, bf16>(a, s);
   if (yf) return launch_gather_direct<bf16, float>(a, s);
@@ -515,18 +768,20 @@ int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
 }
 
 // ---- weight gradient planning ----
+enum { WG_MFMA = 0, WG_THIN_X = 1, WG_THIN_G = 2, WG_DIRECT = 3 };
 struct WgradPlan {
-  bool mfma;
-  int TT, CH, nchunk, nwg, E;
+  int kind;
+  int TT, CH, nchunk, nwg, E, nb;
   size_t lds, ws_bytes;
 };
 
 static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O, int K, int S, int D, int flags) {
   WgradPlan p{};
   const bool anyf32 = (flags & (VQA_X_F32 | VQA_Y_F32)) != 0;
-  p.mfma = !anyf32 && (C == 32 || C == 64) && (O == 32 || O == 64) && K <= 4;
   const size_t esz = dtype == VQA_BF16 ? 2 : 4;
-  if (p.mfma) {
+  p.nb = (flags & WG_DB_FROM_X) ? C : O;
+  if (!anyf32 && (C == 32 || C == 64) && (O == 32 || O == 64) && K <= 4) {
+    p.kind = WG_MFMA;
     p.TT = dtype == VQA_BF16 ? 256 : 128;
     const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
     p.lds = ((size_t)p.TT * (O + 16 / esz) + (size_t)rows_in * (C + 16 / esz)) * esz;
@@ -535,21 +790,30 @@ static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O,
       const int r2 = (p.TT - 1) * S + (K - 1) * D + 1;
       p.lds = ((size_t)p.TT * (O + 16 / esz) + (size_t)r2 * (C + 16 / esz)) * esz;
     }
+  } else if (K <= 4 && C % 8 == 0 && C <= 256 && O <= 2 && !(flags & WG_DB_FROM_X)) {
+    p.kind = WG_THIN_X;
+    p.TT = 64;
+    p.lds = (size_t)256 * (4 * 2 * 8 + 8) * sizeof(float);
+  } else if (K <= 4 && O % 8 == 0 && O <= 256 && C <= 2 && !(flags & WG_DB_FROM_X)) {
+    p.kind = WG_THIN_G;
+    p.TT = 64;
+    p.lds = (size_t)256 * (4 * 2 * 8 + 8) * sizeof(float);
   } else {
+    p.kind = WG_DIRECT;
     p.TT = 64;
     const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
     p.lds = ((size_t)p.TT * O + (size_t)rows_in * C) * 4;
   }
-  // chunk so that the grid has ~1024 workgroups, each at least one sub-tile
-  long long target = 1024;
-  long long per_item = (target + B - 1) / B;
+  // ~512 workgroups (two per CU): each streams its rows once; partials stay small
+  const long long target = 512;
+  const long long per_item = (target + B - 1) / B;
   int ch = (int)((T_out + per_item - 1) / per_item);
   ch = ((ch + p.TT - 1) / p.TT) * p.TT;
   if (ch < p.TT) ch = p.TT;
   p.CH = ch;
   p.nchunk = (T_out + ch - 1) / ch;
   p.nwg = p.nchunk * B;
-  p.E = K * C * O + O;
+  p.E = K * C * O + p.nb;
   p.ws_bytes = (size_t)p.nwg * p.E * sizeof(float);
   return p;
 }
@@ -591,6 +855,24 @@ static int launch_wgrad_direct(const WgradArgs& a, const WgradPlan& p, hipStream
   return VQA_OK;
 }
 
+template <class TX, class TG, bool WX>
+static int launch_wgrad_thin(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds((const void*)wgrad_thin_kernel<TX, TG, WX>, p.lds, &lds_set, "wgrad_thin_kernel");
+  if (rc != VQA_OK) return rc;
+  hipLaunchKernelGGL((wgrad_thin_kernel<TX, TG, WX>), dim3(p.nchunk, a.B), dim3(256), p.lds, s, a);
+  VQA_LAUNCHED("wgrad_thin_kernel");
+  return VQA_OK;
+}
+
+template <bool WX>
+static int launch_wgrad_thin_t(const WgradArgs& a, const WgradPlan& p, bool xf, bool gf, hipStream_t s) {
+  if (xf && gf) return launch_wgrad_thin<float, float, WX>(a, p, s);
+  if (xf) return launch_wgrad_thin<float, bf16, WX>(a, p, s);
+  if (gf) return launch_wgrad_thin<bf16, float, WX>(a, p, s);
+  return launch_wgrad_thin<bf16, bf16, WX>(a, p, s);
+}
+
 int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_in, int T_out, int C, int O, int K,
               int S, int D, int P, int flags, int dtype, void* ws, size_t ws_bytes, hipStream_t s) {
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
@@ -598,52 +880,36 @@ int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_i
   VQA_ARG(B > 0 && T_in > 0 && T_out > 0 && C > 0 && O > 0 && K > 0 && S > 0 && D > 0, "non-positive shape");
   WgradPlan p = plan_wgrad(dtype, B, T_in, T_out, C, O, K, S, D, flags);
   VQA_ARG(ws && ws_bytes >= p.ws_bytes, "workspace too small: need %zu bytes, got %zu", p.ws_bytes, ws_bytes);
-  VQA_REQUIRE(p.lds <= 160 * 1024, VQA_E_UNSUPPORTED, "wgrad: LDS tile too large (%zu B)", p.lds);
-  VQA_REQUIRE(p.mfma || K * C * O <= 16 * 256, VQA_E_UNSUPPORTED, "wgrad: generic path limited to K*C*O<=4096");
-  VQA_REQUIRE(O <= 256 && 256 % O == 0, VQA_E_UNSUPPORTED, "wgrad: C_out must divide 256");
-  WgradArgs a{x, g, (float*)ws, B, T_in, T_out, C, O, K, S, D, P, p.CH, p.nchunk, flags};
+  VQA_REQUIRE(p.lds <= 150 * 1024, VQA_E_UNSUPPORTED, "wgrad: LDS tile too large (%zu B)", p.lds);
+  VQA_REQUIRE(p.kind != WG_DIRECT || K * C * O <= 16 * 256, VQA_E_UNSUPPORTED,
+              "wgrad: generic path limited to K*C*O<=4096");
+  VQA_REQUIRE(p.nb <= 256 && 256 % p.nb == 0, VQA_E_UNSUPPORTED, "wgrad: bias width must divide 256");
+  WgradArgs a{x, g, (float*)ws, B, T_in, T_out, C, O, K, S, D, P, p.CH, p.nchunk, flags, p.nb};
+  const bool xf = dtype == VQA_F32 || (flags & VQA_X_F32);
+  const bool gf = dtype == VQA_F32 || (flags & VQA_Y_F32);
   int rc;
-  if (p.mfma) {
-    rc = dtype == VQA_BF16 ? launch_wgrad_mfma<bf16>(a, p, s) : launch_wgrad_mfma<float>(a, p, s);
-  } else {
-    const bool xf = dtype == VQA_F32 || (flags & VQA_X_F32);
-    const bool gf = dtype == VQA_F32 || (flags & VQA_Y_F32);
-    if (xf && gf) rc = launch_wgrad_direct<float, float>(a, p, s);
-    else if (xf) rc = launch_wgrad_direct<float, bf16>(a, p, s);
-    else if (gf) rc = launch_wgrad_direct<bf16, float>(a, p, s);
-    else rc = launch_wgrad_direct<bf16, bf16>(a, p, s);
+  switch (p.kind) {
+    case WG_MFMA:
+      rc = dtype == VQA_BF16 ? launch_wgrad_mfma<bf16>(a, p, s) : launch_wgrad_mfma<float>(a, p, s);
+      break;
+    case WG_THIN_X: rc = launch_wgrad_thin_t<true>(a, p, xf, gf, s); break;
+    case WG_THIN_G: rc = launch_wgrad_thin_t<false>(a, p, xf, gf, s); break;
+    default:
+      if (xf && gf) rc = launch_wgrad_direct<float, float>(a, p, s);
+      else if (xf) rc = launch_wgrad_direct<float, bf16>(a, p, s);
+      else if (gf) rc = launch_wgrad_direct<bf16, float>(a, p, s);
+      else rc = launch_wgrad_direct<bf16, bf16>(a, p, s);
   }
   if (rc != VQA_OK) return rc;
   const int KCO = K * C * O;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((p.E + 255) / 256), dim3(256), 0, s, (const float*)ws, p.nwg,
-                     p.E, KCO, dw, db);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((p.E + 63) / 64), dim3(256), 0, s, (const float*)ws, p.nwg, p.E,
+                     KCO, dw, db);
   VQA_LAUNCHED("reduce_partials_kernel");
   return VQA_OK;
 }
 
 size_t wgrad_ws(int dtype, int B, int T_in, int T_out, int C, int O, int K, int S, int D, int flags) {
   return plan_wgrad(dtype, B, T_in, T_out, C, O, K, S, D, flags).ws_bytes;
-}
-
-// column-sum (conv-transpose bias gradient): ws must hold nwg*O floats
-static const int kColsumRows = 2048;
-size_t colsum_ws(long long rows, int O) { return (size_t)((rows + kColsumRows - 1) / kColsumRows) * O * sizeof(float); }
-
-int run_colsum(const void* y, long long rows, int O, float* out, int dtype, void* ws, size_t ws_bytes, hipStream_t s) {
-  VQA_REQUIRE(O <= 256 && 256 % O == 0, VQA_E_UNSUPPORTED, "colsum: O must divide 256");
-  const int nwg = (int)((rows + kColsumRows - 1) / kColsumRows);
-  VQA_ARG(ws && ws_bytes >= (size_t)nwg * O * sizeof(float), "colsum workspace too small");
-  if (dtype == VQA_BF16)
-    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, dim3(nwg), dim3(256), 0, s, (const bf16*)y, rows, O, kColsumRows,
-                       (float*)ws);
-  else
-    hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nwg), dim3(256), 0, s, (const float*)y, rows, O, kColsumRows,
-                       (float*)ws);
-  VQA_LAUNCHED("colsum_partial_kernel");
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((O + 255) / 256), dim3(256), 0, s, (const float*)ws, nwg, O, O, out,
-                     (float*)nullptr);
-  VQA_LAUNCHED("reduce_partials_kernel");
-  return VQA_OK;
 }
 
 }  // namespace vqa
@@ -733,10 +999,8 @@ extern "C" int vqa_conv1d_transpose_bwd_data(const void* dy, const float* w, con
 extern "C" size_t vqa_conv1d_transpose_bwd_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K,
                                                             int stride, int pad_left, int flags, int dtype) {
   (void)pad_left;
-  const int f = swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32);
-  size_t a = wgrad_ws(dtype, B, T_out, T_in, C_out, C_in, K, stride, 1, f);
-  size_t b = colsum_ws((long long)B * T_out, C_out);
-  return std::max(a, b);
+  const int f = (swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32)) | WG_DB_FROM_X;
+  return wgrad_ws(dtype, B, T_out, T_in, C_out, C_in, K, stride, 1, f);
 }
 
 extern "C" int vqa_conv1d_transpose_bwd_weight(const void* x, const void* dy, float* dw, float* db, int B, int T_in,
@@ -746,10 +1010,9 @@ extern "C" int vqa_conv1d_transpose_bwd_weight(const void* x, const void* dy, fl
   VQA_REQUIRE(stride == 2 && K == 4 && pad_left == 1, VQA_E_UNSUPPORTED,
               "conv1d_transpose: supports stride 2, K 4, pad_left 1");
   VQA_ARG(T_out == stride * T_in, "conv1d_transpose_bwd_weight: T_out %d != stride*T_in", T_out);
-  // dW[k][co][ci] = sum_i dy[2i + k - 1][co] * x[i][ci]: the gather weight-gradient with dy as input
-  const int f = swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32);
-  int rc = run_wgrad(dy, x, dw, nullptr, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left, f, dtype, workspace,
-                     ws_bytes, (hipStream_t)stream);
-  if (rc != VQA_OK || !db) return rc;
-  return run_colsum(dy, (long long)B * T_out, C_out, db, dtype, workspace, ws_bytes, (hipStream_t)stream);
+  // dW[k][co][ci] = sum_i dy[2i + k - 1][co] * x[i][ci]: the gather weight-gradient with dy as its input;
+  // db[co] = column sums of dy, taken from the same staged rows (WG_DB_FROM_X)
+  const int f = (swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32)) | WG_DB_FROM_X;
+  return run_wgrad(dy, x, dw, db, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left, f, dtype, workspace, ws_bytes,
+                   (hipStream_t)stream);
 }

@@ -98,6 +98,8 @@ def ptr(t: Optional[torch.Tensor]):
         return None
     if not t.is_cuda:
         raise VQAError("libvqa ops take device tensors only (got a CPU tensor)")
+    if not t.is_contiguous():
+        raise VQAError(f"libvqa ops take contiguous (N, T, C) tensors (got strides {t.stride()})")
     return ctypes.c_void_p(t.data_ptr())
 
 

@@ -24,8 +24,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
+import vqa_dp
 import vqa_lib as V
 from data_utils import SpectralTarget, multispectral_loss_and_grad
 from encdec import Decoder, Encoder
@@ -110,17 +110,15 @@ class VQVAE:
         self.hops = [self.T // t for t in self.latent_lens]  # 8 / 32 / 128 at down_depth [3,2,2] (vqvae.py:54)
 
         # all-reduce bucket: [grads (P, padded) | per-level VQ stats | per-level (recon, commit, spectral)]
-        P = (self.store.size + 63) // 64 * 64
-        stats = [vq.stats_size() for vq in self.vqs]
-        self._P = P
-        self.bucket = torch.zeros(P + sum(stats) + 3 * levels, dtype=torch.float32, device=self.device)
+        lay = vqa_dp.bucket_layout(self.store.size, [vq.stats_size() for vq in self.vqs], levels)
+        self.layout = lay
+        P = lay["grads"][1]
+        self.bucket = torch.zeros(lay["total"], dtype=torch.float32, device=self.device)
         self.store.materialize(self.device, grad_buffer=self.bucket[:P], seed=seed)
-        off = P
-        for vq, n in zip(self.vqs, stats):
-            vq.bind_stats(self.bucket[off:off + n])
-            off += n
+        for vq, (a, b) in zip(self.vqs, lay["stats"]):
+            vq.bind_stats(self.bucket[a:b])
         self._stats_region = self.bucket[P:]
-        self.loss_slots = self.bucket[off:].view(levels, 3)
+        self.loss_slots = self.bucket[lay["losses"][0]:lay["losses"][1]].view(levels, 3)
         for l, vq in enumerate(self.vqs):
             vq.commit = self.loss_slots[l, 1:2]
 
@@ -164,28 +162,23 @@ class VQVAE:
         return x.contiguous()
 
     def _world(self) -> int:
-        if dist.is_available() and dist.is_initialized():
-            return dist.get_world_size(self.process_group)
-        return 1
+        return vqa_dp.world_size(self.process_group)
 
     def _rank(self) -> int:
-        if dist.is_available() and dist.is_initialized():
-            return dist.get_rank(self.process_group)
-        return 0
+        return vqa_dp.rank(self.process_group)
 
     # ------------------------------------------------------------------ the step
     def _compute(self, x: torch.Tensor, training_grads: bool):
         """Forward (+ backward when training_grads) of every level; EMA sums into the bucket."""
         self._stats_region.zero_()
-        world, rank = self._world(), self._rank()
         target = SpectralTarget(x)
         B = x.shape[0]
         for l in range(self.levels):
             enc, vq, dec = self.encoders[l], self.vqs[l], self.decoders[l]
             z = enc.forward(x, save=training_grads)
             n_loc = z.shape[0] * z.shape[1]
-            q, _ = vq.forward(z, training=True, row_offset=rank * n_loc, n_global=world * n_loc,
-                              save=training_grads)
+            row_offset, n_global = vqa_dp.global_row_range(n_loc, self.process_group)
+            q, _ = vq.forward(z, training=True, row_offset=row_offset, n_global=n_global, save=training_grads)
             r = dec.forward(q, save=training_grads)
             spec, dr_spec = multispectral_loss_and_grad(target, r)
             self.loss_slots[l, 2].copy_(spec)
@@ -210,8 +203,7 @@ class VQVAE:
         self._macc[:, 1] += 1.0
 
     def _exchange(self):
-        if self._world() > 1:
-            dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM, group=self.process_group)
+        vqa_dp.exchange(self.bucket, self.process_group)
 
     def results(self) -> Dict[str, torch.Tensor]:
         res = self._macc[:, 0] / self._macc[:, 1].clamp(min=1.0)
