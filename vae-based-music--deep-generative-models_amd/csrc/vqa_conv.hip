@@ -127,15 +127,14 @@ __global__ __launch_bounds__(256) void gather_thin_kernel(GatherArgs a) {
   __syncthreads();
   const TX* X = (const TX*)a.x;
   const int OG = a.O / OV;
-  const long long total = (long long)a.B * a.T_out * OG;
+  const int total = a.B * a.T_out * OG;  // < 2^31 (host-checked)
   const bool relu = a.flags & VQA_PRE_RELU;
   const bool vec = (a.C % 8) == 0;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int og = (int)(e % OG);
-    const long long r = e / OG;
-    const int t = (int)(r % a.T_out);
-    const int n = (int)(r / a.T_out);
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int og = e % OG;
+    const int r = e / OG;
+    const int t = r % a.T_out;
+    const int n = r / a.T_out;
     float acc[OV];
 #pragma unroll
     for (int q = 0; q < OV; ++q) acc[q] = 0.f;
@@ -241,12 +240,138 @@ __device__ __forceinline__ void stage_rows(T* xl, int XS, const T* Xi, int lo, i
   }
 }
 
-// MFMA gather conv. One workgroup = 4 waves = TM output rows of one item x all O channels.
+// Narrow-output gather conv (O <= 8, C in {32, 64}; the decoder output conv C=64 -> O=1): one block =
+// TB output rows of one item; the input rows are staged through LDS with coalesced 16-byte loads and
+// every thread reduces one output row from LDS.
+template <class TX, class TY, int C>
+__global__ __launch_bounds__(256) void gather_thinO_kernel(GatherArgs a, int ntb) {
+  constexpr int TB = 256;
+  constexpr int XS = C + 16 / (int)sizeof(TX);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* wl = (float*)smem;  // [K][C][O]
+  const int KCO = a.K * C * a.O;
+  TX* xl = (TX*)(smem + ((KCO * 4 + 15) / 16) * 16);
+  const int n = blockIdx.x / ntb, t0 = (blockIdx.x - n * ntb) * TB;
+  for (int e = threadIdx.x; e < KCO; e += 256) {
+    const int o = e % a.O, c = (e / a.O) % C, k = e / (a.O * C);
+    wl[e] = weff(a, k, c, o);
+  }
+  const int rows_in = (TB - 1) * a.S + (a.K - 1) * a.D + 1;
+  stage_rows<TX, C>(xl, XS, (const TX*)a.x + (long long)n * a.T_in * C, 0, a.T_in, t0 * a.S - a.P, rows_in,
+                    a.flags & VQA_PRE_RELU);
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= a.T_out) return;
+  float acc[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) acc[o] = 0.f;
+  for (int k = 0; k < a.K; ++k) {
+    const TX* xr = xl + (threadIdx.x * a.S + k * a.D) * XS;
+    const float* wk = wl + k * C * a.O;
+#pragma unroll
+    for (int c0 = 0; c0 < C; c0 += 8) {
+      float xv[8];
+      ld8_(xr + c0, xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+          if (o < a.O) acc[o] += xv[j] * wk[(c0 + j) * a.O + o];
+    }
+  }
+  const long long oi = out_index(a, n, t, 0);
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    if (o < a.O) {
+      float v = acc[o];
+      if (a.bias) v = v + a.bias[o];
+      if (a.flags & VQA_POST_MASK) v = ld((const TY*)a.mask + oi + o) > 0.f ? v : 0.f;
+      if (a.flags & VQA_ADD_RESIDUAL) v = ld((const TY*)a.resid + oi + o) + v;
+      st((TY*)a.y + oi + o, v);
+    }
+  }
+}
+
+template <class T> struct Raw4;
+template <> struct Raw4<bf16> { typedef bf16x4 type; };
+template <> struct Raw4<float> { typedef f32x4 type; };
+
+// Register-staged row loader (issue early, write late — cdna_hip_programming.md T14): chunk
+// e = threadIdx.x + i*256 of a rows x C tile, 16 B each, PV chunks per thread held in VGPRs; chunks
+// beyond 256*PV are staged synchronously by tail().
+template <class T, int C, int PV>
+struct RowStager {
+  static constexpr int VEC = 16 / (int)sizeof(T), CPR = C / VEC;
+  uint4 v[PV];
+  __device__ __forceinline__ void load(const T* Xi, int lo, int hi, int r0, int rows) {
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      uint4 t = {0u, 0u, 0u, 0u};
+      if (e < rows * CPR) {
+        const int rr = e / CPR, q = e - rr * CPR, ti = r0 + rr;
+        if (ti >= lo && ti < hi) t = *((const uint4*)(Xi + (long long)ti * C) + q);
+      }
+      v[i] = t;
+    }
+  }
+  __device__ __forceinline__ void store(T* xl, int XS, int rows, bool relu) {
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < rows * CPR) {
+        const int rr = e / CPR, q = e - rr * CPR;
+        uint4 t = v[i];
+        if (relu) relu_bits<T>(t);
+        *(uint4*)(xl + rr * XS + q * VEC) = t;
+      }
+    }
+  }
+  __device__ __forceinline__ void tail(T* xl, int XS, const T* Xi, int lo, int hi, int r0, int rows, bool relu) {
+    for (int e = threadIdx.x + PV * 256; e < rows * CPR; e += 256) {
+      const int rr = e / CPR, q = e - rr * CPR, ti = r0 + rr;
+      uint4 t = {0u, 0u, 0u, 0u};
+      if (ti >= lo && ti < hi) t = *((const uint4*)(Xi + (long long)ti * C) + q);
+      if (relu) relu_bits<T>(t);
+      *(uint4*)(xl + rr * XS + q * VEC) = t;
+    }
+  }
+};
+
+// Weights -> LDS image [K][O][C + pad] in T, with all global loads of a batch issued before any store.
+template <class T, int C, int O>
+__device__ __forceinline__ void stage_weights(const GatherArgs& a, T* wl, int WS) {
+  const int KOC = a.K * O * C;
+  for (int e0 = 0; e0 < KOC; e0 += 256 * 8) {
+    float wv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = e0 + threadIdx.x + j * 256;
+      wv[j] = 0.f;
+      if (e < KOC) {
+        const int c = e % C, o = (e / C) % O, k = e / (C * O);
+        wv[j] = weff(a, k, c, o);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = e0 + threadIdx.x + j * 256;
+      if (e < KOC) {
+        const int c = e % C, o = (e / C) % O, k = e / (C * O);
+        wl[(k * O + o) * WS + c] = (T)wv[j];
+      }
+    }
+  }
+}
+
+// MFMA gather conv, persistent: each workgroup (4 waves) owns a contiguous range of TM-row tiles (so a
+// tile's halo rows were just read by its predecessor on the same CU), stages the weights once, and
+// prefetches tile i+1's input rows into registers while tile i runs its MFMAs and epilogue.
 // D[o][t] = sum_{k,c} Weff^T[o][(k,c)] * X[(k,c)][t]: the A operand is the weight (rows = output
 // channels), the B operand a 16-byte channel run of one input row, so each lane of the accumulator
 // holds 4 consecutive output channels of one time step (8- or 16-byte stores).
-template <class T, int C, int O, int TM>
-__global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a) {
+template <class T, int C, int O, int TM, int PV>
+__global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   typedef Mfma<T> M;
   constexpr int NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
   constexpr int XS = C + lds_pad<T>();
@@ -256,70 +381,105 @@ __global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a) {
   T* wl = (T*)smem;
   T* xl = wl + (size_t)a.K * O * WS;
 
-  const int n = blockIdx.y;
-  const int t0 = blockIdx.x * TM;
   const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
-
-  for (int e = threadIdx.x; e < a.K * O * C; e += blockDim.x) {
-    const int c = e % C, o = (e / C) % O, k = e / (C * O);
-    wl[(k * O + o) * WS + c] = (T)weff(a, k, c, o);
-  }
-  stage_rows<T, C>(xl, XS, (const T*)a.x + (long long)n * a.T_in * C, 0, a.T_in, t0 * a.S - a.P, rows_in,
-                   a.flags & VQA_PRE_RELU);
-  __syncthreads();
-
+  const int tbeg = blockIdx.x * tpw, tend = min(ntiles, tbeg + tpw);
+  if (tbeg >= tend) return;
+  const T* X = (const T*)a.x;
+  const bool relu = a.flags & VQA_PRE_RELU;
+  const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ko = M::koff(lane);
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k = 0; k < a.K; ++k) {
-    const T* wk = wl + (size_t)k * O * WS + (lane & 15) * WS + ko;
-    const T* xk = xl + (size_t)(k * a.D) * XS + ko;
-#pragma unroll
-    for (int cc = 0; cc < C; cc += M::KS) {
-      typename M::frag af[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) af[mt] = M::load(wk + mt * 16 * WS + cc);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int tl = wave * RW + nt * 16 + (lane & 15);
-        const typename M::frag bf = M::load(xk + (size_t)(tl * a.S) * XS + cc);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = M::mma(af[mt], bf, acc[mt][nt]);
-      }
-    }
+  stage_weights<T, C, O>(a, wl, WS);
+  RowStager<T, C, PV> stg;
+  {
+    const int n = tbeg / ntm, t0 = (tbeg - n * ntm) * TM;
+    const T* Xi = X + (long long)n * a.T_in * C;
+    stg.load(Xi, 0, a.T_in, t0 * a.S - a.P, rows_in);
+    stg.store(xl, XS, rows_in, relu);
+    stg.tail(xl, XS, Xi, 0, a.T_in, t0 * a.S - a.P, rows_in, relu);
   }
+  __syncthreads();
 
-  const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
+  for (int tile = tbeg; tile < tend; ++tile) {
+    const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
+    // epilogue operands of THIS tile first (older than the prefetch in the vmcnt queue)
+    typedef typename Raw4<T>::type R4;
+    R4 mk[MT][NT], rs[MT][NT];
+    int oidx[MT][NT];  // < 2^31 elements per tensor (host-checked)
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int t = t0 + wave * RW + nt * 16 + (lane & 15);
-    if (t >= a.T_out) continue;
+    for (int nt = 0; nt < NT; ++nt) {
+      const int t = t0 + wave * RW + nt * 16 + (lane & 15);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int o = mt * 16 + 4 * (lane >> 4);
-      const long long oi = out_index(a, n, t, o);
-      if (oi < 0) continue;
-      f32x4 v = acc[mt][nt];
-      if (a.bias) {
-        const float* bp = a.bias + bias_index(a, o);
-        v = f32x4{v[0] + bp[0], v[1] + bp[1], v[2] + bp[2], v[3] + bp[3]};
+      for (int mt = 0; mt < MT; ++mt) {
+        const int o = mt * 16 + 4 * (lane >> 4);
+        const int oi = t < a.T_out ? (int)out_index(a, n, t, o) : -1;
+        oidx[mt][nt] = oi;
+        if (do_mask && oi >= 0) mk[mt][nt] = *(const R4*)((const T*)a.mask + oi);
+        if (do_res && oi >= 0) rs[mt][nt] = *(const R4*)((const T*)a.resid + oi);
       }
-      if (do_mask) {
-        const f32x4 m = ld4((const T*)a.mask + oi);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
-      }
-      if (do_res) {
-        const f32x4 r = ld4((const T*)a.resid + oi);
-        v = f32x4{r[0] + v[0], r[1] + v[1], r[2] + v[2], r[3] + v[3]};
-      }
-      st4((T*)a.y + oi, v);
     }
+    const bool has_next = tile + 1 < tend;
+    int nn = 0, nt0 = 0;
+    if (has_next) {
+      nn = (tile + 1) / ntm;
+      nt0 = (tile + 1 - nn * ntm) * TM;
+      stg.load(X + (long long)nn * a.T_in * C, 0, a.T_in, nt0 * a.S - a.P, rows_in);
+    }
+
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < a.K; ++k) {
+      const T* wk = wl + (size_t)k * O * WS + (lane & 15) * WS + ko;
+      const T* xk = xl + (size_t)(k * a.D) * XS + ko;
+#pragma unroll
+      for (int cc = 0; cc < C; cc += M::KS) {
+        typename M::frag af[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) af[mt] = M::load(wk + mt * 16 * WS + cc);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int tl = wave * RW + nt * 16 + (lane & 15);
+          const typename M::frag bf = M::load(xk + (size_t)(tl * a.S) * XS + cc);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = M::mma(af[mt], bf, acc[mt][nt]);
+        }
+      }
+    }
+
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int oi = oidx[mt][nt];
+        if (oi < 0) continue;
+        const int o = mt * 16 + 4 * (lane >> 4);
+        f32x4 v = acc[mt][nt];
+        if (a.bias) {
+          const float* bp = a.bias + bias_index(a, o);
+          v = f32x4{v[0] + bp[0], v[1] + bp[1], v[2] + bp[2], v[3] + bp[3]};
+        }
+        if (do_mask) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (float)mk[mt][nt][i] > 0.f ? v[i] : 0.f;
+        }
+        if (do_res) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (float)rs[mt][nt][i] + v[i];
+        }
+        st4((T*)a.y + oi, v);
+      }
+    }
+    __syncthreads();  // every wave is done reading xl
+    if (has_next) {
+      const T* Xi = X + (long long)nn * a.T_in * C;
+      stg.store(xl, XS, rows_in, relu);
+      stg.tail(xl, XS, Xi, 0, a.T_in, nt0 * a.S - a.P, rows_in, relu);
+    }
+    __syncthreads();
   }
 }
 
@@ -370,12 +530,30 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
   const int NB = db_x ? C : O;
   const int dbo = threadIdx.x % NB, dbr = threadIdx.x / NB, dbstep = 256 / NB;
 
+  const bool relu = a.flags & VQA_PRE_RELU;
+  const T* Gi = (const T*)a.g + (long long)n * a.T_out * O;
+  const T* Xi = (const T*)a.x + (long long)n * a.T_in * C;
+  RowStager<T, O, 4> sg;
+  RowStager<T, C, 4> sx;
+  if (tbeg < tend) {
+    const int nrows = min(TT, tend - tbeg);
+    sg.load(Gi, tbeg, tbeg + nrows, tbeg, TT);
+    sx.load(Xi, 0, a.T_in, tbeg * a.S - a.P, rows_in);
+    sg.store(gl, GS, TT, false);
+    sg.tail(gl, GS, Gi, tbeg, tbeg + nrows, tbeg, TT, false);
+    sx.store(xl, XS, rows_in, relu);
+    sx.tail(xl, XS, Xi, 0, a.T_in, tbeg * a.S - a.P, rows_in, relu);
+  }
+  __syncthreads();
   for (int t0 = tbeg; t0 < tend; t0 += TT) {
     const int nrows = min(TT, tend - t0);
-    stage_rows<T, O>(gl, GS, (const T*)a.g + (long long)n * a.T_out * O, t0, t0 + nrows, t0, TT, false);
-    stage_rows<T, C>(xl, XS, (const T*)a.x + (long long)n * a.T_in * C, 0, a.T_in, t0 * a.S - a.P, rows_in,
-                     a.flags & VQA_PRE_RELU);
-    __syncthreads();
+    const int t1 = t0 + TT;
+    const bool has_next = t1 < tend;
+    const int nrows1 = has_next ? min(TT, tend - t1) : 0;
+    if (has_next) {  // prefetch the next sub-tile while this one is reduced
+      sg.load(Gi, t1, t1 + nrows1, t1, TT);
+      sx.load(Xi, 0, a.T_in, t1 * a.S - a.P, rows_in);
+    }
     if (db_x) {
       for (int r = a.P + dbr; r < a.P + nrows * a.S; r += dbstep) dbacc += (float)xl[r * XS + dbo];
     } else {
@@ -396,6 +574,13 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
         }
         acc[ti] = c;
       }
+    }
+    __syncthreads();
+    if (has_next) {
+      sg.store(gl, GS, TT, false);
+      sg.tail(gl, GS, Gi, t1, t1 + nrows1, t1, TT, false);
+      sx.store(xl, XS, rows_in, relu);
+      sx.tail(xl, XS, Xi, 0, a.T_in, t1 * a.S - a.P, rows_in, relu);
     }
     __syncthreads();
   }
@@ -477,47 +662,63 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
   if (rl < RL) {
-    for (int t = tbeg + rl; t < tend; t += RL) {
-      if (WIDE_X) {
-        float gv[NM];
+    // two rows per iteration, all loads issued before the FMAs (memory-level parallelism)
+    for (int t = tbeg + rl; t < tend; t += 2 * RL) {
+      float gv[2][WIDE_X ? NM : 8];
+      float xv[2][KM][WIDE_X ? 8 : NM];
 #pragma unroll
-        for (int i = 0; i < NM; ++i) gv[i] = i < NN ? ld(G + (long long)t * a.O + i) : 0.f;
-        if (v == 0)
+      for (int u = 0; u < 2; ++u) {
+        const int tt = t + u * RL;
+        const bool okr = tt < tend;
+        if (WIDE_X) {
 #pragma unroll
-          for (int i = 0; i < NM; ++i) bacc[i] += gv[i];
+          for (int i = 0; i < NM; ++i) gv[u][i] = (okr && i < NN) ? ld(G + (long long)tt * a.O + i) : 0.f;
+        } else {
+          if (okr) ld8(G + (long long)tt * a.O + v * 8, gv[u]);
+          else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[u][j] = 0.f;
+        }
 #pragma unroll
         for (int k = 0; k < KM; ++k) {
-          const int ti = t * a.S + k * a.D - a.P;
-          if (k < a.K && ti >= 0 && ti < a.T_in) {
-            float xv[8];
-            ld8(X + (long long)ti * a.C + v * 8, xv);
+          const int ti = tt * a.S + k * a.D - a.P;
+          const bool ok = okr && k < a.K && ti >= 0 && ti < a.T_in;
+          if (WIDE_X) {
+            if (ok) ld8(X + (long long)ti * a.C + v * 8, xv[u][k]);
+            else
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              if (relu) xv[j] = fmaxf(xv[j], 0.f);
+              for (int j = 0; j < 8; ++j) xv[u][k][j] = 0.f;
+          } else {
 #pragma unroll
-              for (int i = 0; i < NM; ++i) acc[k][i][j] += xv[j] * gv[i];
-            }
+            for (int i = 0; i < NM; ++i) xv[u][k][i] = (ok && i < NN) ? ld(X + (long long)ti * a.C + i) : 0.f;
           }
         }
-      } else {
-        float gv[8];
-        ld8(G + (long long)t * a.O + v * 8, gv);
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bacc[j] += gv[j];
+      for (int u = 0; u < 2; ++u) {
+        if (WIDE_X) {
+          if (v == 0)
 #pragma unroll
-        for (int k = 0; k < KM; ++k) {
-          const int ti = t * a.S + k * a.D - a.P;
-          if (k < a.K && ti >= 0 && ti < a.T_in) {
+            for (int i = 0; i < NM; ++i) bacc[i] += gv[u][i];
+#pragma unroll
+          for (int k = 0; k < KM; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float x = relu ? fmaxf(xv[u][k][j], 0.f) : xv[u][k][j];
+#pragma unroll
+              for (int i = 0; i < NM; ++i) acc[k][i][j] += x * gv[u][i];
+            }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bacc[j] += gv[u][j];
+#pragma unroll
+          for (int k = 0; k < KM; ++k)
 #pragma unroll
             for (int i = 0; i < NM; ++i) {
-              if (i < NN) {
-                float xs = ld(X + (long long)ti * a.C + i);
-                if (relu) xs = fmaxf(xs, 0.f);
+              const float x = relu ? fmaxf(xv[u][k][i], 0.f) : xv[u][k][i];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[k][i][j] += xs * gv[j];
-              }
+              for (int j = 0; j < 8; ++j) acc[k][i][j] += x * gv[u][j];
             }
-          }
         }
       }
     }
@@ -662,36 +863,50 @@ static int ensure_dyn_lds(const void* fn, size_t bytes, size_t* cached, const ch
   *cached = bytes;
   return VQA_OK;
 }
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// rows per workgroup tile: all O channels x TM rows; TM keeps VGPRs <= ~128 (3 waves/SIMD)
 static int gather_tm(int O, int S) {
-  if (O == 32) return S == 1 ? 256 : 128;
-  if (O == 64) return 128;
-  return 64;
+  (void)S;
+  return O == 32 ? 128 : 64;
 }
 
 template <class T, int C, int O, int TM>
 static int launch_gather_mfma_t(const GatherArgs& a, hipStream_t s) {
-  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>();
+  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>(), PV = 8;
   const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
   const size_t lds = ((size_t)a.K * O * WS + (size_t)rows_in * XS) * sizeof(T);
   VQA_REQUIRE(lds <= 160 * 1024, VQA_E_UNSUPPORTED, "gather conv: LDS tile too large (%zu B)", lds);
+  VQA_REQUIRE((long long)a.B * (a.wmode == W_PAIR ? a.T_full * (O / 2) : (long long)a.T_out * O) < (1ll << 31),
+              VQA_E_UNSUPPORTED, "gather conv: output tensor exceeds 2^31 elements");
   static size_t lds_set = 0;
-  const int rc = ensure_dyn_lds((const void*)gather_mfma_kernel<T, C, O, TM>, lds, &lds_set, "gather_mfma_kernel");
+  const int rc = ensure_dyn_lds((const void*)gather_mfma_kernel<T, C, O, TM, PV>, lds, &lds_set, "gather_mfma_kernel");
   if (rc != VQA_OK) return rc;
-  dim3 grid((a.T_out + TM - 1) / TM, a.B);
-  hipLaunchKernelGGL((gather_mfma_kernel<T, C, O, TM>), grid, dim3(256), lds, s, a);
+  const int ntm = (a.T_out + TM - 1) / TM;
+  const int ntiles = ntm * a.B;
+  int per_cu = (int)((160 * 1024) / lds);
+  per_cu = per_cu < 1 ? 1 : (per_cu > 3 ? 3 : per_cu);
+  int nwg = num_cus() * per_cu;
+  if (nwg > ntiles) nwg = ntiles;
+  const int tpw = (ntiles + nwg - 1) / nwg;
+  nwg = (ntiles + tpw - 1) / tpw;
+  hipLaunchKernelGGL((gather_mfma_kernel<T, C, O, TM, PV>), dim3(nwg), dim3(256), lds, s, a, ntm, ntiles, tpw);
   VQA_LAUNCHED("gather_mfma_kernel");
   return VQA_OK;
 }
 
 template <class T, int C, int O>
 static int launch_gather_mfma_o(const GatherArgs& a, hipStream_t s) {
-  const int tm = gather_tm(O, a.S);
-  if (O == 32) {
-    if (tm == 256) return launch_gather_mfma_t<T, C, O, 256>(a, s);
-    return launch_gather_mfma_t<T, C, O, 128>(a, s);
-  }
-  if (O == 64) return launch_gather_mfma_t<T, C, O, 128>(a, s);
-  return launch_gather_mfma_t<T, C, O, 64>(a, s);
+  if constexpr (O == 32) return launch_gather_mfma_t<T, C, O, 128>(a, s);
+  else return launch_gather_mfma_t<T, C, O, 64>(a, s);
 }
 
 template <class T>
@@ -728,8 +943,27 @@ static int launch_gather_direct(const GatherArgs& a, hipStream_t s) {
   return VQA_OK;
 }
 
+template <class TX, class TY, int C>
+static int launch_gather_thinO_c(const GatherArgs& a, hipStream_t s) {
+  const int ntb = (a.T_out + 255) / 256;
+  const int rows_in = 255 * a.S + (a.K - 1) * a.D + 1;
+  const size_t lds = ((size_t)a.K * C * a.O * 4 + 15) / 16 * 16 + (size_t)rows_in * (C + 16 / sizeof(TX)) * sizeof(TX);
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds((const void*)gather_thinO_kernel<TX, TY, C>, lds, &lds_set, "gather_thinO_kernel");
+  if (rc != VQA_OK) return rc;
+  hipLaunchKernelGGL((gather_thinO_kernel<TX, TY, C>), dim3(ntb * a.B), dim3(256), lds, s, a, ntb);
+  VQA_LAUNCHED("gather_thinO_kernel");
+  return VQA_OK;
+}
+
+template <class TX, class TY>
+static int launch_gather_thinO(const GatherArgs& a, hipStream_t s) {
+  return a.C == 32 ? launch_gather_thinO_c<TX, TY, 32>(a, s) : launch_gather_thinO_c<TX, TY, 64>(a, s);
+}
+
 template <class TX, class TY>
 static int launch_gather_thin(const GatherArgs& a, hipStream_t s) {
+  VQA_REQUIRE((long long)a.B * a.T_out * a.O < (1ll << 31), VQA_E_UNSUPPORTED, "thin conv: tensor too large");
   const int OV = (a.O % 8 == 0) ? 8 : 1;
   const long long total = (long long)a.B * a.T_out * (a.O / OV);
   long long blocks = (total + 255) / 256;
@@ -754,6 +988,12 @@ int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
   if (mfma_ok(a)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
   const bool xf = dtype == VQA_F32 || (a.flags & VQA_X_F32);
   const bool yf = dtype == VQA_F32 || (a.flags & VQA_Y_F32);
+  if (a.O <= 8 && (a.C == 32 || a.C == 64) && a.wmode != W_PAIR && a.K <= 4 && a.S <= 2 && a.D <= 64) {
+    if (xf && yf) return launch_gather_thinO<float, float>(a, s);
+    if (xf) return launch_gather_thinO<float, bf16>(a, s);
+    if (yf) return launch_gather_thinO<bf16, float>(a, s);
+    return launch_gather_thinO<bf16, bf16>(a, s);
+  }
   if ((a.C <= 8 || a.O <= 8) && (size_t)a.K * a.C * a.O * 4 <= 64 * 1024 &&
       (a.wmode != W_PAIR || (a.O / 2) % 8 == 0 || a.O % 8 != 0)) {
     if (xf && yf) return launch_gather_thin<float, float>(a, s);
@@ -782,7 +1022,7 @@ static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O,
   p.nb = (flags & WG_DB_FROM_X) ? C : O;
   if (!anyf32 && (C == 32 || C == 64) && (O == 32 || O == 64) && K <= 4) {
     p.kind = WG_MFMA;
-    p.TT = dtype == VQA_BF16 ? 256 : 128;
+    p.TT = dtype == VQA_BF16 ? 128 : 64;
     const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
     p.lds = ((size_t)p.TT * (O + 16 / esz) + (size_t)rows_in * (C + 16 / esz)) * esz;
     if (p.lds > 150 * 1024) {
@@ -804,8 +1044,9 @@ static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O,
     const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
     p.lds = ((size_t)p.TT * O + (size_t)rows_in * C) * 4;
   }
-  // ~512 workgroups (two per CU): each streams its rows once; partials stay small
-  const long long target = 512;
+  // ~512 workgroups (two per CU) for the MFMA kinds: each streams its rows once and partials stay
+  // small; the thin kinds have tiny partials and short per-row work, so they take 2048.
+  const long long target = (p.kind == WG_THIN_X || p.kind == WG_THIN_G) ? 2048 : 512;
   const long long per_item = (target + B - 1) / B;
   int ch = (int)((T_out + per_item - 1) / per_item);
   ch = ((ch + p.TT - 1) / p.TT) * p.TT;
@@ -830,7 +1071,6 @@ static int launch_wgrad_mfma_t(const WgradArgs& a, const WgradPlan& p, hipStream
 
 template <class T, int C, int O>
 static int launch_wgrad_mfma_co(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
-  if (p.TT == 256) return launch_wgrad_mfma_t<T, C, O, 256>(a, p, s);
   if (p.TT == 128) return launch_wgrad_mfma_t<T, C, O, 128>(a, p, s);
   return launch_wgrad_mfma_t<T, C, O, 64>(a, p, s);
 }
