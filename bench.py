@@ -33,7 +33,7 @@ METRIC = "audio-samples/sec/GPU VQ-VAE train step, 44.1kHz 65536-frame chunks @1
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CFG2 = dict(levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2], num_embeddings=2048,
             residual_width=32, residual_depth=4, dilation_factor=3)
-DOMINANT = "gather_mfma_kernel<bf16, C=32, O=32, TM=256>"  # resblock forwards + stride-1 data-gradients
+DOMINANT = "gather_mfma_kernel<bf16, C=32, O=32, TM=128>"  # resblock forwards + stride-1 data-gradients
 
 
 def parse():

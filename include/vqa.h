@@ -87,6 +87,30 @@ int vqa_conv1d_transpose_bwd_weight(const void* x, const void* dy, float* dw, fl
 size_t vqa_conv1d_transpose_bwd_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K,
                                                  int stride, int pad_left, int flags, int dtype);
 
+/* ---- deferred weight-gradient reduction -------------------------------------------------------------
+ * The *_partials variants of the two bwd_weight calls write per-workgroup partial sums into the caller's
+ * workspace and fill *desc (host memory) instead of reducing; one vqa_reduce_partials call later reduces
+ * any number of them in a single launch (fixed summation order: deterministic). The workspaces must
+ * stay allocated until that call has executed on the stream. */
+typedef struct {
+  const float* partials; /* workspace written by the *_partials call                      */
+  float* dw;             /* destination of elements [0, n_w)                                  */
+  float* db;             /* destination of elements [n_w, n) (bias), may be NULL              */
+  int nparts;            /* partial rows                                                      */
+  int n;                 /* elements per partial row                                          */
+  int n_w;               /* weight elements per partial row                                   */
+  int reserved;
+} vqa_partials_desc;
+int vqa_conv1d_bwd_weight_partials(const void* x, const void* dy, float* dw, float* db, int B, int T_in, int T_out,
+                                   int C_in, int C_out, int K, int stride, int dilation, int pad_left, int flags,
+                                   int dtype, void* workspace, size_t ws_bytes, vqa_partials_desc* desc,
+                                   vqa_stream_t stream);
+int vqa_conv1d_transpose_bwd_weight_partials(const void* x, const void* dy, float* dw, float* db, int B, int T_in,
+                                             int T_out, int C_in, int C_out, int K, int stride, int pad_left,
+                                             int flags, int dtype, void* workspace, size_t ws_bytes,
+                                             vqa_partials_desc* desc, vqa_stream_t stream);
+int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vqa_stream_t stream);
+
 /* ---- Vector quantizer (VectorQuantizer.py) ---------------------------------------------------- */
 /* e_sqnorm[k] = sum_d E[d][k]^2  (VectorQuantizer.py:180). E is (D, K). */
 int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream);

@@ -9,7 +9,9 @@ enc0/blk0/res2/rb1 gives 2.7e-3 there while every other block is at 1e-7). The s
 test_every_conv_call_teacher_forced / test_resblock_backward_teacher_forced: every conv call (and every
 residual block) of a real step against fp64 autograd on the GPU's own inputs and ReLU masks — no branch
 can flip; bound 1e-5 relative L2 (fp32 accumulation over up to ~2^17 rows; measured <= 2.3e-6).
-Weights and codebooks after two Adam/EMA steps: relative L2 <= 1e-3; usage counts N_t equal on >= 99 %
+Each step starts the oracle from the GPU model's state (weights, Adam moments, codebook state), so the
+second step is held to the same bounds as the first; the GPU's Adam update is checked against keras_adam
+in fp64 on the GPU's own gradients (rel 1e-6). Codebooks after two EMA steps: relative L2 <= 1e-3; usage counts N_t equal on >= 99 %
 of codes (a code can move only when a row sits on a near-tie). bf16 model: losses rel
 <= 3e-2, gradient relative L2 <= 0.15 per tensor.
 """
@@ -63,6 +65,39 @@ def _check_grads(grads, ref_grads, l2_tol, med_tol, tag):
     assert med < med_tol, f"{tag}: median max-norm grad error {med:.3e}"
 
 
+def _sync_oracle(ref, m):
+    """Teacher-force the oracle onto the GPU model's state: weights, Adam moments, codebook state."""
+    sd = m.state_dict()
+    flat = sd["weights"].double()
+    am = sd.get("adam_m")
+    av = sd.get("adam_v")
+    for n in ref.names:
+        off, shape = m.store.offsets[n]
+        cnt = int(np.prod(shape))
+        ref.p[n] = flat[off:off + cnt].reshape(shape).clone().requires_grad_(True)
+        if am is not None:
+            ref.adam_m[n] = am[off:off + cnt].double().reshape(shape).clone()
+            ref.adam_v[n] = av[off:off + cnt].double().reshape(shape).clone()
+    for l, st in enumerate(sd["vq"]):
+        ref.vq[l] = {k: torch.tensor(np.asarray(st[k]), dtype=torch.float64) for k in ("embeddings", "m_t", "N_t")}
+        ref.vq[l]["calls"] = int(st["calls"])
+
+
+def _check_adam(m, before, t):
+    """The GPU's Adam step on its own gradients vs keras_adam in fp64 (TF ApplyAdam form)."""
+    after = m.state_dict()
+    g = m.store.grad[:m.store.size].detach().cpu().double()
+    w0 = before["weights"].double()
+    m0 = before["adam_m"].double() if "adam_m" in before else torch.zeros_like(w0)
+    v0 = before["adam_v"].double() if "adam_v" in before else torch.zeros_like(w0)
+    w, mm, vv = R.keras_adam(w0, g, m0, v0, t)
+    scale = {"w": w0.abs() + 1e-2, "m": mm.abs() + g.abs() + m0.abs(), "v": vv + g * g + v0}
+    for got, want, tag in ((after["weights"], w, "w"), (after["adam_m"], mm, "m"), (after["adam_v"], vv, "v")):
+        err = (got.double() - want).abs()
+        # fp32 arithmetic: a few ulp of the operands (w: of |w| and of the 1e-3-sized update)
+        assert bool((err <= 1e-6 * scale[tag] + 1e-30).all()), f"adam step {t} {tag}: max err {float(err.max()):.3e}"
+
+
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_train_step_fp32_matches_oracle(cuda, name):
     c = CONFIGS[name]
@@ -74,6 +109,10 @@ def test_train_step_fp32_matches_oracle(cuda, name):
     x1 = R.synthetic_batch(B, cfg.input_len, seed=12)
     hist = []
     for step, x in enumerate((x0, x1)):
+        # every step starts the oracle from the GPU's state, so step 1 is checked as strictly as step 0
+        # (free-running, Adam turns fp32 rounding in near-zero gradients into +-lr weight moves)
+        _sync_oracle(ref, m)
+        before = m.state_dict()
         out = ref.train_step(x)
         hist.append(out)
         res = {k: float(v) for k, v in m.train_step(x).items()}
@@ -83,10 +122,8 @@ def test_train_step_fp32_matches_oracle(cuda, name):
             tol = 1e-5 if "usage" not in k and "entropy" not in k else 2e-2
             assert abs(res[k] - want) <= tol * max(abs(want), 1e-3), f"step {step} {k}: gpu {res[k]} oracle {want}"
         _check_grads(m.store.grads(), ref.last["grads"], 5e-3, 5e-4, f"step {step}")
-    w = m.get_weights()
-    ow, ovq = ref.state_numpy()
-    for n in ow:
-        assert _l2(w[n], ow[n]) < 1e-3, f"weight {n}"
+        _check_adam(m, before, step + 1)
+    ovq = ref.state_numpy()[1]
     for l, st in enumerate(m.get_vq_state()):
         o = ovq[l]
         same = np.isclose(st["N_t"], o["N_t"], rtol=1e-6, atol=1e-6)
@@ -244,7 +281,7 @@ def test_product_against_golden_micro(cuda):
         res = {k: float(v) for k, v in m.train_step(z[f"x{s}"]).items()}
         want = {k: float(np.mean([meta["metrics"][i][k] for i in range(s + 1)])) for k in res}
         for k in res:
-            tol = 1e-5 if "usage" not in k and "entropy" not in k else 2e-2
+            tol = (1e-5 if s == 0 else 5e-5) if "usage" not in k and "entropy" not in k else 2e-2
             assert abs(res[k] - want[k]) <= tol * max(abs(want[k]), 1e-3), (s, k, res[k], want[k])
         g = m.store.grads()
         meds = [_rel(g[n[len(f"grad{s}/"):]], z[n]) for n in z.files if n.startswith(f"grad{s}/")]
@@ -286,10 +323,7 @@ def _spy_convs(monkeypatch):
             rec = {"kind": kind, "layer": self, "args": [host(a) if isinstance(a, torch.Tensor) else a for a in args],
                    "kw": {k: host(v) if isinstance(v, torch.Tensor) else v for k, v in kw.items()},
                    "out": host(out)}
-            if meth == "backward_weight":
-                rec["dw"] = self.store.grad_view(f"{self.name}/kernel").double().cpu().clone()
-                rec["db"] = self.store.grad_view(f"{self.name}/bias").double().cpu().clone()
-            log.append(rec)
+            log.append(rec)  # weight gradients are read after the step (their reduction is deferred)
             return out
         monkeypatch.setattr(cls, meth, f)
 
@@ -312,6 +346,11 @@ def test_every_conv_call_teacher_forced(cuda, monkeypatch, name, dtype):
     m.train_step(R.synthetic_batch(B, cfg.input_len, seed=11))
     monkeypatch.undo()
     assert log
+    g = m.store.grads()
+    for rec in log:
+        if rec["kind"][1] == "backward_weight":
+            rec["dw"] = torch.from_numpy(g[f"{rec['layer'].name}/kernel"]).double()
+            rec["db"] = torch.from_numpy(g[f"{rec['layer'].name}/bias"]).double()
     worst = 0.0
     for rec in log:
         tag, meth = rec["kind"]

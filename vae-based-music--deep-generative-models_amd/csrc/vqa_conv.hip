@@ -303,16 +303,18 @@ template <class T, int C, int PV>
 struct RowStager {
   static constexpr int VEC = 16 / (int)sizeof(T), CPR = C / VEC;
   uint4 v[PV];
+  unsigned ok;
+  // branch-free issue (see TileRegs::load); requires lo < hi (a non-empty row range)
   __device__ __forceinline__ void load(const T* Xi, int lo, int hi, int r0, int rows) {
+    ok = 0u;
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const int e = threadIdx.x + i * 256;
-      uint4 t = {0u, 0u, 0u, 0u};
-      if (e < rows * CPR) {
-        const int rr = e / CPR, q = e - rr * CPR, ti = r0 + rr;
-        if (ti >= lo && ti < hi) t = *((const uint4*)(Xi + (long long)ti * C) + q);
-      }
-      v[i] = t;
+      const int rr = e / CPR, q = e - rr * CPR, ti = r0 + rr;
+      const bool val = e < rows * CPR && ti >= lo && ti < hi;
+      const int tc = val ? ti : lo;
+      v[i] = *((const uint4*)(Xi + (long long)tc * C) + (val ? q : 0));
+      ok |= val ? (1u << i) : 0u;
     }
   }
   __device__ __forceinline__ void store(T* xl, int XS, int rows, bool relu) {
@@ -322,6 +324,7 @@ struct RowStager {
       if (e < rows * CPR) {
         const int rr = e / CPR, q = e - rr * CPR;
         uint4 t = v[i];
+        if (!(ok & (1u << i))) t = uint4{0u, 0u, 0u, 0u};
         if (relu) relu_bits<T>(t);
         *(uint4*)(xl + rr * XS + q * VEC) = t;
       }
@@ -364,14 +367,86 @@ __device__ __forceinline__ void stage_weights(const GatherArgs& a, T* wl, int WS
   }
 }
 
-// MFMA gather conv, persistent: each workgroup (4 waves) owns a contiguous range of TM-row tiles (so a
-// tile's halo rows were just read by its predecessor on the same CU), stages the weights once, and
-// prefetches tile i+1's input rows into registers while tile i runs its MFMAs and epilogue.
-// D[o][t] = sum_{k,c} Weff^T[o][(k,c)] * X[(k,c)][t]: the A operand is the weight (rows = output
-// channels), the B operand a 16-byte channel run of one input row, so each lane of the accumulator
-// holds 4 consecutive output channels of one time step (8- or 16-byte stores).
+// One tile's global -> LDS copy in 16-byte chunks, held in registers between load() and store():
+// chunks [0, nx) are the input rows (with halo; padded LDS rows, compile-time chunks per row), then ne
+// chunks of the ReLU' mask and ne of the residual — the output rows of the tile, contiguous in global
+// memory, copied chunk-linearly (unpadded) into their LDS tiles. Chunk e = threadIdx.x + i*256.
+struct TileSrc {
+  const char* x;      // this item's input row 0
+  int r0, nx;         // first input row of the tile, input chunks
+  const char* m;      // mask bytes of the tile's first output row (nullptr: unused)
+  const char* r;      // residual bytes of the tile's first output row (nullptr: unused)
+  int ne, elim;       // chunks per epilogue tensor; bytes valid from m / r (rows past the item read 0)
+};
+
+template <class T, int C, int PV>
+struct TileRegs {
+  static constexpr int VEC = 16 / (int)sizeof(T), CPR = C / VEC;
+  uint4 v[PV];
+  unsigned ok;  // bit i: chunk i is real data (else it is stored as zeros)
+  // Branch-free: every chunk issues its load (an out-of-range chunk reads a valid dummy address and is
+  // zeroed at store time) so the PV loads go out back to back. A per-chunk `if (valid) load` makes hipcc
+  // branch around each load and wait vmcnt(0) per chunk (cdna_hip_programming.md, trap (c)).
+  __device__ __forceinline__ void load(const TileSrc& s, int T_in) {
+    ok = 0u;
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      const int row = e / CPR, q = e % CPR, gr = s.r0 + row;
+      const bool in_x = e < s.nx;
+      const bool vx = in_x && gr >= 0 && gr < T_in;
+      const int e2 = e - s.nx;
+      const bool in_m = s.m != nullptr && e2 < s.ne;
+      const int e3 = s.m != nullptr ? e2 - s.ne : e2;
+      const int ei = in_m ? e2 : e3;
+      const char* eb = in_m ? s.m : s.r;
+      const bool ve = !in_x && eb != nullptr && ei < s.ne && ei * 16 < s.elim;
+      const char* px = s.x + (long long)gr * C * (int)sizeof(T) + q * 16;
+      const char* pe = eb + (long long)ei * 16;
+      const char* p = vx ? px : (ve ? pe : s.x);
+      v[i] = *(const uint4*)p;
+      ok |= (vx || ve) ? (1u << i) : 0u;
+    }
+  }
+  __device__ __forceinline__ void store(const TileSrc& s, T* xl, int XS, char* ml, char* rl, bool relu) {
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      uint4 t = v[i];
+      if (!(ok & (1u << i))) t = uint4{0u, 0u, 0u, 0u};
+      if (e < s.nx) {
+        const int row = e / CPR, q = e % CPR;
+        if (relu) relu_bits<T>(t);
+        *(uint4*)(xl + row * XS + q * VEC) = t;
+      } else {
+        int e2 = e - s.nx;
+        char* b = s.m ? ml : nullptr;
+        if (!b || e2 >= s.ne) {
+          if (s.m) e2 -= s.ne;
+          b = s.r ? rl : nullptr;
+        }
+        if (b && e2 < s.ne) *((uint4*)b + e2) = t;
+      }
+    }
+  }
+};
+
+// MFMA gather conv, persistent and software-pipelined. Each workgroup (4 waves) owns a contiguous range
+// of TM-row tiles of one or more items (a tile's halo rows were just read by its predecessor on the
+// same CU), stages the weights once, and keeps TWO tiles in flight in registers (tiles i+1, i+2) while
+// tile i runs its MFMAs and epilogue out of LDS — so neither the input rows nor the epilogue operands
+// (residual, ReLU' mask) are ever waited for inside a tile (cdna_hip_programming.md T14, two deep).
+// D[o][t] = sum_{k,c} Weff^T[o][(k,c)] * X[(k,c)][t]: A = weights (rows = output channels), B = a 16-byte
+// channel run of one input row; each accumulator lane holds 4 consecutive output channels of one row.
+// occupancy target: 4 waves/SIMD (<= 128 VGPRs) for the 4-chunk stager, 3 (<= 168) for 8, 2 for 12;
+// O = 128 tiles (and fp32 O = 64 with 8 chunks) need more registers than that without spilling
+template <class T, int O, int PV> constexpr int gather_waves() {
+  return (O >= 128 || (sizeof(T) == 4 && O >= 64 && PV > 4)) ? 2 : (PV <= 4 ? 4 : (PV <= 8 ? 3 : 2));
+}
+
 template <class T, int C, int O, int TM, int PV>
-__global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gather_waves<T, O, PV>(), 8)))
+void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   typedef Mfma<T> M;
   constexpr int NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
   constexpr int XS = C + lds_pad<T>();
@@ -380,53 +455,52 @@ __global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a, int ntm,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* wl = (T*)smem;
   T* xl = wl + (size_t)a.K * O * WS;
-
   const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
+  // epilogue tiles, unpadded and chunk-linear: [TM][O], or in PAIR mode [2TM][O/2] (full-resolution rows)
+  T* ml = xl + (size_t)rows_in * XS;
+  T* rl = ml + (size_t)TM * O;
+
   const int tbeg = blockIdx.x * tpw, tend = min(ntiles, tbeg + tpw);
   if (tbeg >= tend) return;
-  const T* X = (const T*)a.x;
-  const bool relu = a.flags & VQA_PRE_RELU;
+  const bool pair = a.wmode == W_PAIR;
   const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
+  const bool relu = a.flags & VQA_PRE_RELU;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ko = M::koff(lane);
+  constexpr int ESZ = (int)sizeof(T);
+  const int erow = pair ? O / 2 : O;  // elements per output row (full resolution)
+
+  auto source = [&](int tile) {
+    const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
+    TileSrc src;
+    src.x = (const char*)a.x + (long long)n * a.T_in * C * ESZ;
+    src.r0 = t0 * a.S - a.P;
+    src.nx = rows_in * (C * ESZ / 16);
+    const int r0e = pair ? 2 * t0 : t0;                 // first output row of the tile
+    const int rvalid = pair ? a.T_full : a.T_out;        // output rows of this item
+    const long long eoff = ((long long)n * rvalid + r0e) * erow * ESZ;
+    src.m = do_mask ? (const char*)a.mask + eoff : nullptr;
+    src.r = do_res ? (const char*)a.resid + eoff : nullptr;
+    src.ne = TM * O * ESZ / 16;
+    src.elim = (rvalid - r0e) * erow * ESZ;
+    return src;
+  };
 
   stage_weights<T, C, O>(a, wl, WS);
-  RowStager<T, C, PV> stg;
-  {
-    const int n = tbeg / ntm, t0 = (tbeg - n * ntm) * TM;
-    const T* Xi = X + (long long)n * a.T_in * C;
-    stg.load(Xi, 0, a.T_in, t0 * a.S - a.P, rows_in);
-    stg.store(xl, XS, rows_in, relu);
-    stg.tail(xl, XS, Xi, 0, a.T_in, t0 * a.S - a.P, rows_in, relu);
+  TileSrc S0, S1;
+  TileRegs<T, C, PV> A, B;
+  S0 = source(tbeg);
+  A.load(S0, a.T_in);
+  if (tbeg + 1 < tend) {
+    S1 = source(tbeg + 1);
+    B.load(S1, a.T_in);
   }
+  A.store(S0, xl, XS, (char*)ml, (char*)rl, relu);
   __syncthreads();
 
-  for (int tile = tbeg; tile < tend; ++tile) {
+  // one tile: MFMAs out of LDS, epilogue operands out of LDS, stores to global
+  auto run_tile = [&](int tile) {
     const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
-    // epilogue operands of THIS tile first (older than the prefetch in the vmcnt queue)
-    typedef typename Raw4<T>::type R4;
-    R4 mk[MT][NT], rs[MT][NT];
-    int oidx[MT][NT];  // < 2^31 elements per tensor (host-checked)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int t = t0 + wave * RW + nt * 16 + (lane & 15);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int o = mt * 16 + 4 * (lane >> 4);
-        const int oi = t < a.T_out ? (int)out_index(a, n, t, o) : -1;
-        oidx[mt][nt] = oi;
-        if (do_mask && oi >= 0) mk[mt][nt] = *(const R4*)((const T*)a.mask + oi);
-        if (do_res && oi >= 0) rs[mt][nt] = *(const R4*)((const T*)a.resid + oi);
-      }
-    }
-    const bool has_next = tile + 1 < tend;
-    int nn = 0, nt0 = 0;
-    if (has_next) {
-      nn = (tile + 1) / ntm;
-      nt0 = (tile + 1 - nn * ntm) * TM;
-      stg.load(X + (long long)nn * a.T_in * C, 0, a.T_in, nt0 * a.S - a.P, rows_in);
-    }
-
     f32x4 acc[MT][NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -449,36 +523,64 @@ __global__ __launch_bounds__(256) void gather_mfma_kernel(GatherArgs a, int ntm,
         }
       }
     }
-
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
+      const int tl = wave * RW + nt * 16 + (lane & 15);
+      const int t = t0 + tl;
+      if (t >= a.T_out) continue;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int oi = oidx[mt][nt];
-        if (oi < 0) continue;
         const int o = mt * 16 + 4 * (lane >> 4);
+        const long long oi = out_index(a, n, t, o);
+        if (oi < 0) continue;
+        // this element inside the staged (unpadded) epilogue tile
+        int eidx;
+        if (pair) {
+          const int Ob = O / 2, p = o >= Ob ? 1 : 0;
+          eidx = (2 * tl + p) * Ob + (o - p * Ob);
+        } else {
+          eidx = tl * O + o;
+        }
         f32x4 v = acc[mt][nt];
         if (a.bias) {
           const float* bp = a.bias + bias_index(a, o);
           v = f32x4{v[0] + bp[0], v[1] + bp[1], v[2] + bp[2], v[3] + bp[3]};
         }
         if (do_mask) {
+          const f32x4 m = ld4(ml + eidx);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = (float)mk[mt][nt][i] > 0.f ? v[i] : 0.f;
+          for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
         }
         if (do_res) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = (float)rs[mt][nt][i] + v[i];
+          const f32x4 r = ld4(rl + eidx);
+          v = f32x4{r[0] + v[0], r[1] + v[1], r[2] + v[2], r[3] + v[3]};
         }
         st4((T*)a.y + oi, v);
       }
     }
-    __syncthreads();  // every wave is done reading xl
-    if (has_next) {
-      const T* Xi = X + (long long)nn * a.T_in * C;
-      stg.store(xl, XS, rows_in, relu);
-      stg.tail(xl, XS, Xi, 0, a.T_in, nt0 * a.S - a.P, rows_in, relu);
+  };
+
+  // steady state, unrolled by two so each register set has a static name (rule 20)
+  for (int tile = tbeg; tile < tend; tile += 2) {
+    // LDS: tile; B: tile+1 (in flight); A: free
+    if (tile + 2 < tend) {
+      S0 = source(tile + 2);
+      A.load(S0, a.T_in);
     }
+    run_tile(tile);
+    __syncthreads();
+    if (tile + 1 >= tend) break;
+    B.store(S1, xl, XS, (char*)ml, (char*)rl, relu);
+    __syncthreads();
+    // LDS: tile+1; A: tile+2 (in flight); B: free
+    if (tile + 3 < tend) {
+      S1 = source(tile + 3);
+      B.load(S1, a.T_in);
+    }
+    run_tile(tile + 1);
+    __syncthreads();
+    if (tile + 2 >= tend) break;
+    A.store(S0, xl, XS, (char*)ml, (char*)rl, relu);
     __syncthreads();
   }
 }
@@ -847,6 +949,47 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, i
   }
 }
 
+// Batched form: one launch reduces up to kMaxDescs layers; block b belongs to the descriptor whose
+// [start, start + ceil(n/64)) range contains it. Same fixed summation order as reduce_partials_kernel.
+constexpr int kMaxDescs = 48;
+struct ReduceBatch {
+  vqa_partials_desc d[kMaxDescs];
+  int start[kMaxDescs + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void reduce_partials_batched_kernel(ReduceBatch rb) {
+  __shared__ float red[4][64];
+  int i = 0;
+  while (i + 1 < rb.count && (int)blockIdx.x >= rb.start[i + 1]) ++i;
+  const vqa_partials_desc& d = rb.d[i];
+  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = ((int)blockIdx.x - rb.start[i]) * 64 + el;
+  const int E = d.n, nparts = d.nparts;
+  const float* ws = d.partials;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (e < E) {
+    int p = grp;
+    for (; p + 12 < nparts; p += 16) {
+      s0 += ws[(size_t)p * E + e];
+      s1 += ws[(size_t)(p + 4) * E + e];
+      s2 += ws[(size_t)(p + 8) * E + e];
+      s3 += ws[(size_t)(p + 12) * E + e];
+    }
+    for (; p < nparts; p += 4) s0 += ws[(size_t)p * E + e];
+  }
+  red[grp][el] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (grp == 0 && e < E) {
+    const float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+    if (e < d.n_w) {
+      if (d.dw) d.dw[e] = s;
+    } else if (d.db) {
+      d.db[e - d.n_w] = s;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 // Raise a kernel's dynamic-LDS limit only when a launch needs more than the 64 KiB default; the value is
@@ -879,21 +1022,27 @@ static int gather_tm(int O, int S) {
   return O == 32 ? 128 : 64;
 }
 
-template <class T, int C, int O, int TM>
-static int launch_gather_mfma_t(const GatherArgs& a, hipStream_t s) {
-  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>(), PV = 8;
-  const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
-  const size_t lds = ((size_t)a.K * O * WS + (size_t)rows_in * XS) * sizeof(T);
-  VQA_REQUIRE(lds <= 160 * 1024, VQA_E_UNSUPPORTED, "gather conv: LDS tile too large (%zu B)", lds);
-  VQA_REQUIRE((long long)a.B * (a.wmode == W_PAIR ? a.T_full * (O / 2) : (long long)a.T_out * O) < (1ll << 31),
-              VQA_E_UNSUPPORTED, "gather conv: output tensor exceeds 2^31 elements");
+template <class T, int C, int O, int TM, int PV>
+static int launch_gather_mfma_pv(const GatherArgs& a, size_t lds, hipStream_t s) {
   static size_t lds_set = 0;
   const int rc = ensure_dyn_lds((const void*)gather_mfma_kernel<T, C, O, TM, PV>, lds, &lds_set, "gather_mfma_kernel");
   if (rc != VQA_OK) return rc;
   const int ntm = (a.T_out + TM - 1) / TM;
   const int ntiles = ntm * a.B;
-  int per_cu = (int)((160 * 1024) / lds);
-  per_cu = per_cu < 1 ? 1 : (per_cu > 3 ? 3 : per_cu);
+  // persistent grid = exactly the resident workgroups (VGPR- and LDS-limited), so no workgroup waits
+  // for a second round
+  static int per_cu = 0;
+  static size_t per_cu_lds = 0;
+  if (per_cu == 0 || per_cu_lds != lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)gather_mfma_kernel<T, C, O, TM, PV>, 256, lds) !=
+            hipSuccess || nb < 1) {
+      (void)hipGetLastError();
+      nb = 1;
+    }
+    per_cu = nb;
+    per_cu_lds = lds;
+  }
   int nwg = num_cus() * per_cu;
   if (nwg > ntiles) nwg = ntiles;
   const int tpw = (ntiles + nwg - 1) / nwg;
@@ -901,6 +1050,27 @@ static int launch_gather_mfma_t(const GatherArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((gather_mfma_kernel<T, C, O, TM, PV>), dim3(nwg), dim3(256), lds, s, a, ntm, ntiles, tpw);
   VQA_LAUNCHED("gather_mfma_kernel");
   return VQA_OK;
+}
+
+template <class T, int C, int O, int TM>
+static int launch_gather_mfma_t(const GatherArgs& a, hipStream_t s) {
+  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>(), ES = O + lds_pad<T>();
+  const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
+  const bool pair = a.wmode == W_PAIR;
+  const int nep = ((a.flags & VQA_POST_MASK) ? 1 : 0) + ((a.flags & VQA_ADD_RESIDUAL) ? 1 : 0);
+  const size_t ebytes = (size_t)TM * O * sizeof(T);
+  (void)pair;
+  (void)ES;
+  const size_t lds = ((size_t)a.K * O * WS + (size_t)rows_in * XS) * sizeof(T) + 2 * ebytes;
+  VQA_REQUIRE(lds <= 160 * 1024, VQA_E_UNSUPPORTED, "gather conv: LDS tile too large (%zu B)", lds);
+  // 16-byte chunks per tile held in registers per thread
+  const long long chunks = (long long)rows_in * C * sizeof(T) / 16 + (long long)nep * TM * O * sizeof(T) / 16;
+  const int pv = (int)((chunks + 255) / 256);
+  if (pv <= 4) return launch_gather_mfma_pv<T, C, O, TM, 4>(a, lds, s);
+  if (pv <= 8) return launch_gather_mfma_pv<T, C, O, TM, 8>(a, lds, s);
+  if (pv <= 12) return launch_gather_mfma_pv<T, C, O, TM, 12>(a, lds, s);
+  vqa::set_error("gather conv: tile of %lld chunks exceeds the register stager", chunks);
+  return VQA_E_UNSUPPORTED;
 }
 
 template <class T, int C, int O>
@@ -924,11 +1094,14 @@ static int launch_gather_mfma(const GatherArgs& a, hipStream_t s) {
   return VQA_E_UNSUPPORTED;
 }
 
-static bool mfma_ok(const GatherArgs& a) {
+static bool mfma_ok(const GatherArgs& a, int dtype) {
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return false;
   if (!((a.C == 32 || a.C == 64) && (a.O == 32 || a.O == 64 || a.O == 128))) return false;
   const int tm = gather_tm(a.O, a.S);
   const int rows_in = (tm - 1) * a.S + (a.K - 1) * a.D + 1;
+  const int nep = ((a.flags & VQA_POST_MASK) ? 1 : 0) + ((a.flags & VQA_ADD_RESIDUAL) ? 1 : 0);
+  const int esz = dtype == VQA_BF16 ? 2 : 4;
+  if ((long long)rows_in * a.C * esz / 16 + (long long)nep * tm * a.O * esz / 16 > 12 * 256) return false;
   return (size_t)rows_in * (a.C + 8) * 4 + (size_t)a.K * a.O * (a.C + 8) * 4 <= 150 * 1024;
 }
 
@@ -985,7 +1158,7 @@ int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
           "non-positive shape");
   VQA_ARG(!(a.flags & VQA_POST_MASK) || a.mask, "VQA_POST_MASK without mask");
   VQA_ARG(!(a.flags & VQA_ADD_RESIDUAL) || a.resid, "VQA_ADD_RESIDUAL without residual");
-  if (mfma_ok(a)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
+  if (mfma_ok(a, dtype)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
   const bool xf = dtype == VQA_F32 || (a.flags & VQA_X_F32);
   const bool yf = dtype == VQA_F32 || (a.flags & VQA_Y_F32);
   if (a.O <= 8 && (a.C == 32 || a.C == 64) && a.wmode != W_PAIR && a.K <= 4 && a.S <= 2 && a.D <= 64) {
@@ -1114,7 +1287,8 @@ static int launch_wgrad_thin_t(const WgradArgs& a, const WgradPlan& p, bool xf, 
 }
 
 int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_in, int T_out, int C, int O, int K,
-              int S, int D, int P, int flags, int dtype, void* ws, size_t ws_bytes, hipStream_t s) {
+              int S, int D, int P, int flags, int dtype, void* ws, size_t ws_bytes, hipStream_t s,
+              vqa_partials_desc* defer) {
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
   VQA_ARG(x && g && dw, "null tensor pointer");
   VQA_ARG(B > 0 && T_in > 0 && T_out > 0 && C > 0 && O > 0 && K > 0 && S > 0 && D > 0, "non-positive shape");
@@ -1142,6 +1316,10 @@ int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_i
   }
   if (rc != VQA_OK) return rc;
   const int KCO = K * C * O;
+  if (defer) {
+    *defer = vqa_partials_desc{(const float*)ws, dw, db, p.nwg, p.E, KCO, 0};
+    return VQA_OK;
+  }
   hipLaunchKernelGGL(reduce_partials_kernel, dim3((p.E + 63) / 64), dim3(256), 0, s, (const float*)ws, p.nwg, p.E,
                      KCO, dw, db);
   VQA_LAUNCHED("reduce_partials_kernel");
@@ -1211,7 +1389,8 @@ extern "C" int vqa_conv1d_bwd_weight(const void* x, const void* dy, float* dw, f
                                      int dtype, void* workspace, size_t ws_bytes, vqa_stream_t stream) {
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_weight: T_out %d != ceil(T_in/stride)", T_out);
   return run_wgrad(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
-                   flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, (hipStream_t)stream);
+                   flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, (hipStream_t)stream,
+                   nullptr);
 }
 
 extern "C" int vqa_conv1d_transpose_fwd(const void* x, const float* w, const float* bias, const void* residual,
@@ -1254,5 +1433,50 @@ extern "C" int vqa_conv1d_transpose_bwd_weight(const void* x, const void* dy, fl
   // db[co] = column sums of dy, taken from the same staged rows (WG_DB_FROM_X)
   const int f = (swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32)) | WG_DB_FROM_X;
   return run_wgrad(dy, x, dw, db, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left, f, dtype, workspace, ws_bytes,
-                   (hipStream_t)stream);
+                   (hipStream_t)stream, nullptr);
+}
+
+extern "C" int vqa_conv1d_bwd_weight_partials(const void* x, const void* dy, float* dw, float* db, int B, int T_in,
+                                              int T_out, int C_in, int C_out, int K, int stride, int dilation,
+                                              int pad_left, int flags, int dtype, void* workspace, size_t ws_bytes,
+                                              vqa_partials_desc* desc, vqa_stream_t stream) {
+  VQA_ARG(desc, "bwd_weight_partials: NULL descriptor");
+  VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_weight: T_out %d != ceil(T_in/stride)", T_out);
+  return run_wgrad(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
+                   flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, (hipStream_t)stream,
+                   desc);
+}
+
+extern "C" int vqa_conv1d_transpose_bwd_weight_partials(const void* x, const void* dy, float* dw, float* db, int B,
+                                                        int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                                                        int pad_left, int flags, int dtype, void* workspace,
+                                                        size_t ws_bytes, vqa_partials_desc* desc,
+                                                        vqa_stream_t stream) {
+  VQA_ARG(desc, "bwd_weight_partials: NULL descriptor");
+  VQA_REQUIRE(stride == 2 && K == 4 && pad_left == 1, VQA_E_UNSUPPORTED,
+              "conv1d_transpose: supports stride 2, K 4, pad_left 1");
+  VQA_ARG(T_out == stride * T_in, "conv1d_transpose_bwd_weight: T_out %d != stride*T_in", T_out);
+  const int f = (swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32)) | WG_DB_FROM_X;
+  return run_wgrad(dy, x, dw, db, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left, f, dtype, workspace, ws_bytes,
+                   (hipStream_t)stream, desc);
+}
+
+extern "C" int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vqa_stream_t stream) {
+  VQA_ARG(count >= 0 && (count == 0 || descs), "reduce_partials: bad descriptor list");
+  for (int base = 0; base < count; base += kMaxDescs) {
+    ReduceBatch rb{};
+    rb.count = count - base < kMaxDescs ? count - base : kMaxDescs;
+    int blocks = 0;
+    for (int i = 0; i < rb.count; ++i) {
+      const vqa_partials_desc& d = descs[base + i];
+      VQA_ARG(d.partials && d.n > 0 && d.nparts > 0 && d.n_w <= d.n, "reduce_partials: bad descriptor %d", base + i);
+      rb.d[i] = d;
+      rb.start[i] = blocks;
+      blocks += (d.n + 63) / 64;
+    }
+    rb.start[rb.count] = blocks;
+    hipLaunchKernelGGL(reduce_partials_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);
+    VQA_LAUNCHED("reduce_partials_batched_kernel");
+  }
+  return VQA_OK;
 }

@@ -28,6 +28,7 @@ class ParamStore:
         self.size = 0
         self.flat: Optional[torch.Tensor] = None
         self.grad: Optional[torch.Tensor] = None
+        self.deferred = None  # a vqa_lib.Deferred while a model step batches its weight-gradient reductions
 
     def add(self, name: str, shape: Tuple[int, ...], init: str) -> str:
         if name in self.offsets:
@@ -151,9 +152,12 @@ class Conv1D:
     def backward_weight(self, x, dy, cdt, pre_relu=False):
         B, T, _ = x.shape
         fl = _flags_for(x, dy.dtype, cdt) | (V.PRE_RELU if pre_relu else 0)
-        V.conv1d_bwd_weight(x, dy, self.store.grad_view(f"{self.name}/kernel"),
-                            self.store.grad_view(f"{self.name}/bias"), B, T, dy.shape[1], self.cin, self.cout, self.K,
-                            self.s, self.d, self.pad(T), fl, V.dtype_code(cdt))
+        args = (x, dy, self.store.grad_view(f"{self.name}/kernel"), self.store.grad_view(f"{self.name}/bias"), B, T,
+                dy.shape[1], self.cin, self.cout, self.K, self.s, self.d, self.pad(T), fl, V.dtype_code(cdt))
+        if self.store.deferred is not None:
+            V.conv1d_bwd_weight_deferred(*args, self.store.deferred)
+        else:
+            V.conv1d_bwd_weight(*args)
 
 
 class Conv1DTranspose:
@@ -200,6 +204,9 @@ class Conv1DTranspose:
 
     def backward_weight(self, x, dy, cdt):
         B, T, _ = x.shape
-        V.conv1d_transpose_bwd_weight(x, dy, self.store.grad_view(f"{self.name}/kernel"),
-                                      self.store.grad_view(f"{self.name}/bias"), B, T, dy.shape[1], self.cin,
-                                      self.cout, self.K, self.s, self.pad(dy.shape[1]), 0, V.dtype_code(cdt))
+        args = (x, dy, self.store.grad_view(f"{self.name}/kernel"), self.store.grad_view(f"{self.name}/bias"), B, T,
+                dy.shape[1], self.cin, self.cout, self.K, self.s, self.pad(dy.shape[1]), 0, V.dtype_code(cdt))
+        if self.store.deferred is not None:
+            V.conv1d_transpose_bwd_weight_deferred(*args, self.store.deferred)
+        else:
+            V.conv1d_transpose_bwd_weight(*args)

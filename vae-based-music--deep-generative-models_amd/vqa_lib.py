@@ -26,11 +26,18 @@ EXPORTED = [
     "vqa_vq_sqnorm", "vqa_vq_argmin", "vqa_vq_quantize", "vqa_vq_quantize_workspace", "vqa_vq_backward",
     "vqa_vq_reset_rows", "vqa_vq_ema_apply", "vqa_reset_perm_index",
     "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_counter_add",
+    "vqa_conv1d_bwd_weight_partials", "vqa_conv1d_transpose_bwd_weight_partials", "vqa_reduce_partials",
 ]
 
 
 class VQAError(RuntimeError):
     pass
+
+
+class PartialsDesc(ctypes.Structure):
+    """vqa_partials_desc (include/vqa.h)."""
+    _fields_ = [("partials", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p),
+                ("nparts", ctypes.c_int), ("n", ctypes.c_int), ("n_w", ctypes.c_int), ("reserved", ctypes.c_int)]
 
 
 _P, _I, _L, _S, _F, _U = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float,
@@ -63,6 +70,9 @@ _SIGS = {
     "vqa_mse_loss_workspace": (_S, [_L]),
     "vqa_adam_keras": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P]),
     "vqa_counter_add": (_I, [_P, _L, _P]),
+    "vqa_conv1d_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
+    "vqa_conv1d_transpose_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONVT + [_P, _S, _P, _P]),
+    "vqa_reduce_partials": (_I, [_P, _I, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -149,6 +159,46 @@ def conv1d_bwd_weight(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dil
     _check(lib().vqa_conv1d_bwd_weight(ptr(x), ptr(dy), ptr(dw), ptr(db), B, T_in, T_out, C_in, C_out, K, stride,
                                        dilation, pad, flags, dtype, ptr(ws), ws.numel(), stream()),
            "vqa_conv1d_bwd_weight")
+
+
+class Deferred:
+    """Collects deferred weight-gradient partials; flush() reduces them all in one launch."""
+
+    def __init__(self):
+        self.descs, self.keep = [], []
+
+    def add(self, desc, ws):
+        self.descs.append(desc)
+        self.keep.append(ws)  # the partials must outlive the reduce launch
+
+    def flush(self):
+        if self.descs:
+            arr = (PartialsDesc * len(self.descs))(*self.descs)
+            _check(lib().vqa_reduce_partials(arr, len(self.descs), stream()), "vqa_reduce_partials")
+        self.descs, self.keep = [], []
+
+
+def conv1d_bwd_weight_deferred(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype,
+                               deferred):
+    n = lib().vqa_conv1d_bwd_weight_workspace(B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype)
+    ws = workspace(n, x.device)
+    d = PartialsDesc()
+    _check(lib().vqa_conv1d_bwd_weight_partials(ptr(x), ptr(dy), ptr(dw), ptr(db), B, T_in, T_out, C_in, C_out, K,
+                                                stride, dilation, pad, flags, dtype, ptr(ws), ws.numel(),
+                                                ctypes.byref(d), stream()), "vqa_conv1d_bwd_weight_partials")
+    deferred.add(d, ws)
+
+
+def conv1d_transpose_bwd_weight_deferred(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype,
+                                         deferred):
+    n = lib().vqa_conv1d_transpose_bwd_weight_workspace(B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype)
+    ws = workspace(n, x.device)
+    d = PartialsDesc()
+    _check(lib().vqa_conv1d_transpose_bwd_weight_partials(ptr(x), ptr(dy), ptr(dw), ptr(db), B, T_in, T_out, C_in,
+                                                          C_out, K, stride, pad, flags, dtype, ptr(ws), ws.numel(),
+                                                          ctypes.byref(d), stream()),
+           "vqa_conv1d_transpose_bwd_weight_partials")
+    deferred.add(d, ws)
 
 
 def conv1d_transpose_fwd(x, w, b, residual, y, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype):

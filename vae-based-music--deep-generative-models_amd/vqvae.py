@@ -171,6 +171,8 @@ class VQVAE:
     def _compute(self, x: torch.Tensor, training_grads: bool):
         """Forward (+ backward when training_grads) of every level; EMA sums into the bucket."""
         self._stats_region.zero_()
+        # weight-gradient partials of every layer are reduced in one launch per level
+        self.store.deferred = V.Deferred() if training_grads else None
         target = SpectralTarget(x)
         B = x.shape[0]
         for l in range(self.levels):
@@ -188,6 +190,8 @@ class VQVAE:
                 dq = dec.backward(dr)
                 dz = vq.backward(dq, n_global=n_loc)
                 enc.backward(dz)
+                self.store.deferred.flush()
+        self.store.deferred = None
 
     def _update(self, apply_grads: bool):
         world = self._world()
