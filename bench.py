@@ -35,7 +35,7 @@ METRIC = "audio-samples/sec/GPU VQ-VAE train step, 44.1kHz 65536-frame chunks @1
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CFG2 = dict(levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2], num_embeddings=2048,
             residual_width=32, residual_depth=4, dilation_factor=3)
-DOMINANT = "gather_mfma_kernel<bf16, C=32, O=32, TM=128>"  # residual-block convs: forwards + data-gradients
+DOMINANT = "conv32_kernel<bf16, C=32, O=32, TM=128>"  # 32-channel convs: forwards + fused data/weight gradients
 
 
 def parse():
@@ -67,13 +67,14 @@ def gather_shape(op, C_in, C_out, stride):
 
 
 class KernelTimer:
-    """Roofline of the dominant kernel, gather_mfma_kernel<bf16, C=32, O=32, TM=128>: record every conv
+    """Roofline of the dominant kernel, conv32_kernel<bf16> (C=32, O=32, TM=128): record every conv
     launch of one step that dispatches to it (with its algorithmic bytes: gather input + output +
     residual + mask, activation dtype), then time each distinct launch as back-to-back copies inside
     a hipGraph replayed on the stream libvqa launches on, bracketed by HIP events (no host gaps, so the
     per-launch average is the kernel's own duration, as rocprofv3 reports it)."""
 
-    OPS = ("conv1d_fwd", "conv1d_bwd_data", "conv1d_transpose_fwd", "conv1d_transpose_bwd_data")
+    OPS = ("conv1d_fwd", "conv1d_bwd_data", "conv1d_transpose_fwd", "conv1d_transpose_bwd_data",
+           "conv1d_bwd_data_weight")
 
     def __init__(self, V):
         self.V = V
@@ -82,7 +83,11 @@ class KernelTimer:
 
     def _dominant(self, op, args):
         V = self.V
-        C_in, C_out, stride, flags, dtype = args[8], args[9], args[11], args[-2], args[-1]
+        if op == "conv1d_bwd_data_weight":  # (dy, w, x, residual, dx, dw, db, B, T_in, T_out, C_in, C_out, K, s, ...)
+            C_in, C_out, stride, flags, dtype = args[10], args[11], args[13], args[16], args[17]
+            op = "conv1d_bwd_data"
+        else:
+            C_in, C_out, stride, flags, dtype = args[8], args[9], args[11], args[-2], args[-1]
         if dtype != V.BF16 or flags & (V.X_F32 | V.Y_F32):
             return False
         return gather_shape(op, C_in, C_out, stride) == (32, 32)
@@ -96,7 +101,7 @@ class KernelTimer:
                     key = (_op,) + tuple(v for v in args if isinstance(v, int))
                     if key in self.calls:
                         self.calls[key][1] += 1
-                    else:
+                    else:  # algorithmic bytes: gather input, output, residual, mask / conv input
                         ts = [t for t in args[:5] if isinstance(t, torch.Tensor) and t.numel() > 4096]
                         self.calls[key] = [args, 1, sum(t.numel() * t.element_size() for t in ts)]
                 return _f(*args)
@@ -115,6 +120,8 @@ class KernelTimer:
         stream = torch.cuda.current_stream()
         for key, (args, cnt, nb) in self.calls.items():
             f = self.orig[key[0]]
+            if key[0] == "conv1d_bwd_data_weight":  # time the kernel alone: leave the partials unreduced
+                f = (lambda *a, _f=f: _f(*a[:-1], self.V.Deferred()))
             per_graph = cnt
             f(*args)
             g = torch.cuda.CUDAGraph()

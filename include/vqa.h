@@ -111,6 +111,20 @@ int vqa_conv1d_transpose_bwd_weight_partials(const void* x, const void* dy, floa
                                              vqa_partials_desc* desc, vqa_stream_t stream);
 int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vqa_stream_t stream);
 
+/* ---- fused backward of one Conv1D whose input x enters through an optional ReLU (resnet.py:12-17: the
+ *      two convs of ResnetConv1DBlock; backward = GradientTape.gradient, vqvae.py:143):
+ *      dx = (conv_data_grad(dy) * (x > 0 if VQA_PRE_RELU)) (+ residual if VQA_ADD_RESIDUAL),
+ *      dw/db = the weight gradient with relu(x) (VQA_PRE_RELU) or x.
+ * Stride-1 convs with 32/64 channels run as ONE kernel that reads dy, x (and residual) once; other shapes
+ * fall back to vqa_conv1d_bwd_data + vqa_conv1d_bwd_weight. desc != NULL defers the weight-gradient
+ * reduction as in the *_partials calls. */
+int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const void* x, const void* residual, void* dx,
+                               float* dw, float* db, int B, int T_in, int T_out, int C_in, int C_out, int K,
+                               int stride, int dilation, int pad_left, int flags, int dtype, void* workspace,
+                               size_t ws_bytes, vqa_partials_desc* desc, vqa_stream_t stream);
+size_t vqa_conv1d_bwd_data_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
+                                            int dilation, int pad_left, int flags, int dtype);
+
 /* ---- Vector quantizer (VectorQuantizer.py) ---------------------------------------------------- */
 /* e_sqnorm[k] = sum_d E[d][k]^2  (VectorQuantizer.py:180). E is (D, K). */
 int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream);

@@ -109,6 +109,36 @@ def test_conv1d_fwd_bwd(cuda, case, dt):
         assert _rel(dW, gW) < tol * 2, f"bwd_weight dW pre_relu={pre_relu}"
         assert _rel(db, gb) < tol * 2, "bwd_weight db"
 
+    # fused data + weight gradient (vqa_conv1d_bwd_data_weight): one kernel for the stride-1 32-channel
+    # convs, the two-call fallback elsewhere; dx must equal the plain data-gradient call bit for bit
+    if Cin > 1:
+        for pre_relu, use_res, deferred in ((True, True, False), (True, False, True), (False, False, False)):
+            Wv = Wq.clone().requires_grad_(True)
+            bv = bq.clone().requires_grad_(True)
+            xv = xq.clone().requires_grad_(True)
+            xin = torch.relu(xv) if pre_relu else xv
+            gx, gW, gb = torch.autograd.grad((ref_conv(xin, Wv, bv, s, d) * dyq).sum(), (xv, Wv, bv))
+            resid = torch.randn(B, T, Cin, generator=g, dtype=torch.float64) if use_res else None
+            rd = resid.to(xdt).to(cuda) if use_res else None
+            dx = torch.empty(B, T, Cin, dtype=xdt, device=cuda)
+            dW = torch.full((K, Cin, Cout), float("nan"), dtype=torch.float32, device=cuda)
+            db = torch.full((Cout,), float("nan"), dtype=torch.float32, device=cuda)
+            fl = flags_x | flags_y | (V.PRE_RELU if pre_relu else 0) | (V.ADD_RESIDUAL if use_res else 0)
+            dfr = V.Deferred() if deferred else None
+            V.conv1d_bwd_data_weight(dyd, Wd, xd, rd, dx, dW, db, B, T, To, Cin, Cout, K, s, d, pl, fl, cd, dfr)
+            if dfr is not None:
+                dfr.flush()
+            ref = gx + (_q(resid, xdt) if use_res else 0)
+            tag = f"fused pre_relu={pre_relu} res={use_res} deferred={deferred}"
+            assert _rel(dx, ref) < tol, f"{tag}: dx"
+            assert _rel(dW, gW) < tol * 2, f"{tag}: dW"
+            assert _rel(db, gb) < tol * 2, f"{tag}: db"
+            dx_plain = torch.empty_like(dx)
+            V.conv1d_bwd_data(dyd, Wd, xd if pre_relu else None, rd, dx_plain, B, T, To, Cin, Cout, K, s, d, pl,
+                              flags_x | flags_y | (V.POST_MASK if pre_relu else 0) | (V.ADD_RESIDUAL if use_res else 0),
+                              cd)
+            assert torch.equal(dx, dx_plain), f"{tag}: dx differs from vqa_conv1d_bwd_data"
+
 
 CONVT_CASES = [
     # (C_in, C_out, B, T_in)

@@ -328,8 +328,9 @@ def _spy_convs(monkeypatch):
         monkeypatch.setattr(cls, meth, f)
 
     for cls, tag in ((L.Conv1D, "conv"), (L.Conv1DTranspose, "convT")):
-        for meth in ("forward", "backward_data", "backward_weight"):
-            wrap(cls, meth, (tag, meth))
+        for meth in ("forward", "backward_data", "backward_weight", "backward_data_weight"):
+            if hasattr(cls, meth):
+                wrap(cls, meth, (tag, meth))
     return log
 
 
@@ -348,7 +349,7 @@ def test_every_conv_call_teacher_forced(cuda, monkeypatch, name, dtype):
     assert log
     g = m.store.grads()
     for rec in log:
-        if rec["kind"][1] == "backward_weight":
+        if rec["kind"][1] in ("backward_weight", "backward_data_weight"):
             rec["dw"] = torch.from_numpy(g[f"{rec['layer'].name}/kernel"]).double()
             rec["db"] = torch.from_numpy(g[f"{rec['layer'].name}/bias"]).double()
     worst = 0.0
@@ -380,6 +381,15 @@ def test_every_conv_call_teacher_forced(cuda, monkeypatch, name, dtype):
             if kw.get("residual") is not None:
                 gx = kw["residual"] + gx
             err = _l2(rec["out"].numpy(), gx.numpy())
+        elif meth == "backward_data_weight":  # fused: dx (ReLU' mask = the conv input) and dW, db
+            dy, x0 = rec["args"][0], rec["args"][1]
+            xv = x0.clone().requires_grad_(True)
+            x = xv * (xv > 0) if kw.get("pre_relu") else xv
+            gx, gW, gb = torch.autograd.grad((f(x, W, b) * dy).sum(), (xv, W, b))
+            if kw.get("residual") is not None:
+                gx = kw["residual"] + gx
+            err = max(_l2(rec["out"].numpy(), gx.numpy()), _l2(rec["dw"].numpy(), gW.numpy()),
+                      _l2(rec["db"].numpy(), gb.numpy()))
         else:
             x, dy = rec["args"][0], rec["args"][1]
             if kw.get("pre_relu"):

@@ -37,7 +37,7 @@ def main():
 
     calls = collections.OrderedDict()  # shape key -> (entry point, args, calls per step)
     names = ["conv1d_fwd", "conv1d_bwd_data", "conv1d_transpose_fwd", "conv1d_transpose_bwd_data",
-             "conv1d_bwd_weight_deferred", "conv1d_transpose_bwd_weight_deferred"]
+             "conv1d_bwd_weight_deferred", "conv1d_transpose_bwd_weight_deferred", "conv1d_bwd_data_weight"]
     orig = {n: getattr(V, n) for n in names}
 
     def wrap(n):
@@ -67,7 +67,7 @@ def main():
         nbytes = sum(t.numel() * t.element_size() for t in args if isinstance(t, torch.Tensor) and t.numel() > 4096)
 
         def run():
-            if n.endswith("_deferred"):
+            if n.endswith("_deferred") or n == "conv1d_bwd_data_weight":
                 orig[n](*args[:-1], V.Deferred())
             else:
                 orig[n](*args)

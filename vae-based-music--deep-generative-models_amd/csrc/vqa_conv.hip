@@ -34,6 +34,10 @@ struct GatherArgs {
   int wmode, Kb, Pb;   // weight mapping; base taps; base pad (PAIR)
   int T_full;          // PAIR: full-resolution rows per item (store guard)
   int flags;
+  // fused weight gradient (stride-1 data-gradient only): `mask` is the conv input u (always staged),
+  // wpart receives one fp32 partial [K*O*C dW | C db] per workgroup, wrelu: dW uses relu(u)
+  float* wpart = nullptr;
+  int wrelu = 0;
 };
 
 __device__ __forceinline__ float weff(const GatherArgs& a, int k, int c, int o) {
@@ -197,6 +201,31 @@ template <> struct Mfma<bf16> {
     for (int j = 0; j < 8; ++j) f[j] = p[j * stride];
     return f;
   }
+  static __device__ __forceinline__ frag ones() {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (bf16)1.0f;
+    return f;
+  }
+  // operand whose K index runs down the rows of a row-major LDS tile: lane l gets rows 8(l>>4) .. +7 of
+  // column l&15 from `o` = &tile[row0][col0] — two ds_read_b64_tr_b16 (cdna_hip_programming.md T10);
+  // the caller keeps EXEC full and the row stride a multiple of 8 bytes
+  static __device__ __forceinline__ frag rows(const bf16* o, int stride) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    const int l = threadIdx.x & 63, i = l & 15;
+    const bf16* a0 = o + (8 * (l >> 4) + (i >> 2)) * stride + 4 * (i & 3);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * stride));
+    frag f;
+    const bf16* pl = (const bf16*)&lo;
+    const bf16* ph = (const bf16*)&hi;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = pl[j];
+      f[j + 4] = ph[j];
+    }
+    return f;
+  }
 };
 template <> struct Mfma<float> {
   static constexpr int KS = 4;
@@ -207,6 +236,11 @@ template <> struct Mfma<float> {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ frag gather(const float* p, int) { return *p; }
+  static __device__ __forceinline__ frag ones() { return 1.0f; }
+  static __device__ __forceinline__ frag rows(const float* o, int stride) {
+    const int l = threadIdx.x & 63;
+    return o[(l >> 4) * stride + (l & 15)];
+  }
 };
 
 template <class T> __device__ __forceinline__ void relu_bits(uint4& v);
@@ -222,6 +256,16 @@ template <> __device__ __forceinline__ void relu_bits<float>(uint4& v) {
 }
 
 template <class T> constexpr int lds_pad() { return 16 / (int)sizeof(T); }
+
+__device__ __forceinline__ bf16x8 relu_frag(bf16x8 f) {
+  uint4 u = *(uint4*)&f;
+  relu_bits<bf16>(u);
+  return *(bf16x8*)&u;
+}
+__device__ __forceinline__ float relu_frag(float f) {
+  const int32_t b = __float_as_int(f);
+  return __int_as_float(b & ~(b >> 31));
+}
 
 // Stage rows [r0, r0+rows) of one item (Xi = that item's row 0, channels C) into LDS with padded row
 // stride XS, zero-filling rows outside [lo, hi), optional ReLU. 16-byte vector loads.
@@ -441,7 +485,8 @@ struct TileRegs {
 // occupancy target: 4 waves/SIMD (<= 128 VGPRs) for the 4-chunk stager, 3 (<= 168) for 8, 2 for 12;
 // O = 128 tiles (and fp32 O = 64 with 8 chunks) need more registers than that without spilling
 template <class T, int O, int PV> constexpr int gather_waves() {
-  return (O >= 128 || (sizeof(T) == 4 && O >= 64 && PV > 4)) ? 2 : (PV <= 4 ? 4 : (PV <= 8 ? 3 : 2));
+  if (O >= 128 || (sizeof(T) == 4 && O >= 64 && PV > 4)) return 2;
+  return PV <= 4 ? 4 : (PV <= 5 ? (O <= 32 ? 4 : 3) : (PV <= 8 ? 3 : 2));
 }
 
 template <class T, int C, int O, int TM, int PV>
@@ -582,6 +627,241 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
     if (tile + 2 >= tend) break;
     A.store(S0, xl, XS, (char*)ml, (char*)rl, relu);
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The 32-channel residual convs (C = O = 32, direct or stride-1 data-gradient weights, any K <= 4,
+// stride 1 or 2) — 80 % of the model's conv traffic — get a leaner kernel than gather_mfma_kernel:
+//  * every global access is a raw buffer access through a per-item descriptor, so the hardware range
+//    check supplies the SAME zero padding and drops stores past the item end (no per-element guards);
+//  * all per-thread chunk offsets are computed once per launch: staging costs one add per 16-byte chunk
+//    and the epilogue tensors (ReLU' mask / conv input, residual) are plain contiguous spans;
+//  * the ReLU is one packed integer max per dword (a bf16 / fp32 is negative iff its int16 / int32 is);
+//  * the tile is held in registers two tiles ahead (T14) exactly as in gather_mfma_kernel.
+// FW additionally accumulates the weight gradient of a stride-1 data-gradient from the staged tiles
+// (vqa_conv1d_bwd_data_weight): epilogue tensor 0 is then the conv input u.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t item_rsrc(const void* base, long long off, unsigned bytes) {
+  const unsigned long long p = (unsigned long long)base + (unsigned long long)off;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+  void* q = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <class T> __device__ __forceinline__ u32x4 relu_chunk(u32x4 v);
+__device__ __forceinline__ unsigned relu_pk_bf16(unsigned w) {
+  const s16x2 z = {0, 0};
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, w), z));
+}
+template <> __device__ __forceinline__ u32x4 relu_chunk<bf16>(u32x4 v) {
+  return u32x4{relu_pk_bf16(v.x), relu_pk_bf16(v.y), relu_pk_bf16(v.z), relu_pk_bf16(v.w)};
+}
+__device__ __forceinline__ unsigned relu_f32_bits(unsigned w) { return (unsigned)max((int)w, 0); }
+template <> __device__ __forceinline__ u32x4 relu_chunk<float>(u32x4 v) {
+  return u32x4{relu_f32_bits(v.x), relu_f32_bits(v.y), relu_f32_bits(v.z), relu_f32_bits(v.w)};
+}
+
+template <class T> __device__ __forceinline__ void store_out4(__amdgpu_buffer_rsrc_t r, int voff, f32x4 v);
+template <> __device__ __forceinline__ void store_out4<bf16>(__amdgpu_buffer_rsrc_t r, int voff, f32x4 v) {
+  bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), r, voff, 0, 0);
+}
+template <> __device__ __forceinline__ void store_out4<float>(__amdgpu_buffer_rsrc_t r, int voff, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
+}
+
+template <class T, int PVX, int NEP, bool FW> constexpr int conv32_waves() {
+  if (FW) return sizeof(T) == 2 ? 3 : 2;
+  return (PVX + NEP * (int)sizeof(T)) <= 7 ? 4 : ((PVX + NEP * (int)sizeof(T)) <= 11 ? 3 : 2);
+}
+
+// x-row byte offset that stays out of range after adding any tile base (|base| < 2^30)
+constexpr int kOOB = -0x40000000;
+
+template <class T, int PVX, int NEP, bool FW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv32_waves<T, PVX, NEP, FW>(), 8)))
+void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
+  typedef Mfma<T> M;
+  constexpr int C = 32, O = 32, TM = 128, NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
+  constexpr int ESZ = (int)sizeof(T), VEC = 16 / ESZ, CPR = C / VEC, ROWB = C * ESZ;
+  constexpr int XS = C + lds_pad<T>(), WS = XS;
+  constexpr int RSTEP = 256 / CPR;  // x rows between a thread's consecutive chunks
+  constexpr int XROWS = RSTEP * PVX;
+  constexpr int ECH = TM * O * ESZ / 16 / 256;  // chunks per thread per epilogue tensor
+  constexpr int EBYTES = TM * O * ESZ;
+  static_assert(NEP >= (FW ? 1 : 0) && NEP <= 2, "epilogue tensors");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* wl = (T*)smem;
+  T* xl = wl + (size_t)a.K * O * WS;
+  char* el = (char*)(xl + (size_t)XROWS * XS);
+
+  const int tbeg = blockIdx.x * tpw, tend = min(ntiles, tbeg + tpw);
+  if (tbeg >= tend) return;
+  const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
+  const bool relu = a.flags & VQA_PRE_RELU;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ko = M::koff(lane);
+  const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
+  // epilogue tensor slots: [mask or conv input (FW)] then [residual]
+  const bool has_m = do_mask || FW;
+  const void* ep0 = has_m ? a.mask : a.resid;
+  const void* ep1 = a.resid;
+  const T* ml = (const T*)el;                                   // valid when has_m
+  const T* rl = (const T*)(el + (has_m ? EBYTES : 0));          // valid when do_res
+  const unsigned xbytes = (unsigned)a.T_in * ROWB, obytes = (unsigned)a.T_out * O * ESZ;
+
+  // per-thread chunk geometry, fixed for the launch
+  const int q = threadIdx.x % CPR, row0 = threadIdx.x / CPR;
+  int gx[PVX];
+#pragma unroll
+  for (int i = 0; i < PVX; ++i) gx[i] = (row0 + i * RSTEP < rows_in) ? (row0 + i * RSTEP) * ROWB + q * 16 : kOOB;
+  const int lx = (row0 * XS) * ESZ + q * 16;  // + i * RSTEP * XS * ESZ
+  const int ge = threadIdx.x * 16;            // + j * 4096 (epilogue chunks)
+
+  u32x4 ra[PVX + NEP * ECH], rb[PVX + NEP * ECH];
+  auto load = [&](u32x4* r, int tile) {
+    const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
+    const __amdgpu_buffer_rsrc_t rx = item_rsrc(a.x, (long long)n * xbytes, xbytes);
+    const int xb = (t0 * a.S - a.P) * ROWB;
+#pragma unroll
+    for (int i = 0; i < PVX; ++i) r[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, gx[i] + xb, 0, 0);
+    if constexpr (NEP > 0) {
+      const int eb = t0 * O * ESZ;
+      const __amdgpu_buffer_rsrc_t r0 = item_rsrc(ep0, (long long)n * obytes, obytes);
+#pragma unroll
+      for (int j = 0; j < ECH; ++j) r[PVX + j] = __builtin_amdgcn_raw_buffer_load_b128(r0, ge + j * 4096 + eb, 0, 0);
+      if constexpr (NEP > 1) {
+        const __amdgpu_buffer_rsrc_t r1 = item_rsrc(ep1, (long long)n * obytes, obytes);
+#pragma unroll
+        for (int j = 0; j < ECH; ++j)
+          r[PVX + ECH + j] = __builtin_amdgcn_raw_buffer_load_b128(r1, ge + j * 4096 + eb, 0, 0);
+      }
+    }
+  };
+  auto store = [&](const u32x4* r) {
+#pragma unroll
+    for (int i = 0; i < PVX; ++i)
+      *(u32x4*)((char*)xl + lx + i * RSTEP * XS * ESZ) = relu ? relu_chunk<T>(r[i]) : r[i];
+#pragma unroll
+    for (int j = 0; j < NEP * ECH; ++j) *(u32x4*)(el + ge + j * 4096) = r[PVX + j];
+  };
+
+  // fused weight gradient accumulators (C = O = 32: wave w owns ci-tile w>>1, co-tile w&1 of every tap)
+  f32x4 wacc[4], wdb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias of this lane's 4 output channels per 16-channel block
+  f32x4 bias[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int o = mt * 16 + 4 * (lane >> 4);
+    bias[mt] = a.bias ? f32x4{a.bias[o], a.bias[o + 1], a.bias[o + 2], a.bias[o + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  stage_weights<T, C, O>(a, wl, WS);
+  load(ra, tbeg);
+  if (tbeg + 1 < tend) load(rb, tbeg + 1);
+  store(ra);
+  __syncthreads();
+
+  auto run_tile = [&](int tile) {
+    const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < a.K; ++k) {
+      const T* wk = wl + (size_t)k * O * WS + (lane & 15) * WS + ko;
+      const T* xk = xl + (size_t)(k * a.D) * XS + ko;
+#pragma unroll
+      for (int cc = 0; cc < C; cc += M::KS) {
+        typename M::frag af[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) af[mt] = M::load(wk + mt * 16 * WS + cc);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int tl = wave * RW + nt * 16 + (lane & 15);
+          const typename M::frag bf = M::load(xk + (size_t)(tl * a.S) * XS + cc);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = M::mma(af[mt], bf, acc[mt][nt]);
+        }
+      }
+    }
+    const __amdgpu_buffer_rsrc_t ry = item_rsrc(a.y, (long long)n * obytes, obytes);
+    const int yb = t0 * O * ESZ;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tl = wave * RW + nt * 16 + (lane & 15);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int o = mt * 16 + 4 * (lane >> 4);
+        const int eidx = tl * O + o;
+        f32x4 v = acc[mt][nt] + bias[mt];
+        if (do_mask) {
+          const f32x4 m = ld4(ml + eidx);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
+        }
+        if (do_res) v = ld4(rl + eidx) + v;
+        store_out4<T>(ry, eidx * ESZ + yb, v);
+      }
+    }
+    if constexpr (FW) {
+      const int it = wave >> 1, jt = wave & 1;
+      const T* up = ml + it * 16;
+      const T* gp = xl + jt * 16;
+#pragma unroll 1
+      for (int kk = 0; kk < TM; kk += M::KS) {
+        typename M::frag af = M::rows(up + (size_t)kk * O, O);
+        if (a.wrelu) af = relu_frag(af);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k < a.K) {
+            const typename M::frag bf = M::rows(gp + (size_t)(kk + (a.K - 1 - k) * a.D) * XS, XS);
+            wacc[k] = M::mma(af, bf, wacc[k]);
+          }
+        }
+        if (it == 0) {
+          const typename M::frag bo = M::rows(gp + (size_t)(kk + a.P) * XS, XS);
+          wdb = M::mma(M::ones(), bo, wdb);
+        }
+      }
+    }
+  };
+
+  for (int tile = tbeg; tile < tend; tile += 2) {
+    // LDS: tile; rb: tile+1 (in flight); ra: free
+    if (tile + 2 < tend) load(ra, tile + 2);
+    run_tile(tile);
+    __syncthreads();
+    if (tile + 1 >= tend) break;
+    store(rb);
+    __syncthreads();
+    if (tile + 3 < tend) load(rb, tile + 3);
+    run_tile(tile + 1);
+    __syncthreads();
+    if (tile + 2 >= tend) break;
+    store(ra);
+    __syncthreads();
+  }
+  if constexpr (FW) {
+    float* out = a.wpart + (size_t)blockIdx.x * (size_t)(a.K * O * C + C);
+    const int it = wave >> 1, jt = wave & 1;
+    const int co = jt * 16 + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < a.K) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[((size_t)k * O + it * 16 + 4 * (lane >> 4) + r) * C + co] = wacc[k][r];
+      }
+    }
+    if (it == 0 && lane < 16) out[a.K * O * C + co] = wdb[0];
   }
 }
 
@@ -1016,57 +1296,70 @@ static int num_cus() {
   return n;
 }
 
+// resident workgroups per CU the persistent grid assumes at most (also bounds the fused-wgrad partials)
+constexpr int kMaxGatherPerCU = 4;
+
 // rows per workgroup tile: all O channels x TM rows; TM keeps VGPRs <= ~128 (3 waves/SIMD)
 static int gather_tm(int O, int S) {
   (void)S;
   return O == 32 ? 128 : 64;
 }
 
-template <class T, int C, int O, int TM, int PV>
-static int launch_gather_mfma_pv(const GatherArgs& a, size_t lds, hipStream_t s) {
-  static size_t lds_set = 0;
-  const int rc = ensure_dyn_lds((const void*)gather_mfma_kernel<T, C, O, TM, PV>, lds, &lds_set, "gather_mfma_kernel");
-  if (rc != VQA_OK) return rc;
-  const int ntm = (a.T_out + TM - 1) / TM;
-  const int ntiles = ntm * a.B;
-  // persistent grid = exactly the resident workgroups (VGPR- and LDS-limited), so no workgroup waits
-  // for a second round
-  static int per_cu = 0;
-  static size_t per_cu_lds = 0;
-  if (per_cu == 0 || per_cu_lds != lds) {
+// persistent grid = the resident workgroups (VGPR- and LDS-limited), so no workgroup waits for a second
+// round; tiles are split into contiguous ranges (a tile's halo rows were just read by its predecessor)
+static int persistent_grid(const void* fn, size_t lds, int* per_cu, size_t* per_cu_lds, int ntiles, int* tpw) {
+  if (*per_cu == 0 || *per_cu_lds != lds) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)gather_mfma_kernel<T, C, O, TM, PV>, 256, lds) !=
-            hipSuccess || nb < 1) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, lds) != hipSuccess || nb < 1) {
       (void)hipGetLastError();
       nb = 1;
     }
-    per_cu = nb;
-    per_cu_lds = lds;
+    *per_cu = nb > kMaxGatherPerCU ? kMaxGatherPerCU : nb;
+    *per_cu_lds = lds;
   }
-  int nwg = num_cus() * per_cu;
+  int nwg = num_cus() * *per_cu;
   if (nwg > ntiles) nwg = ntiles;
-  const int tpw = (ntiles + nwg - 1) / nwg;
-  nwg = (ntiles + tpw - 1) / tpw;
+  *tpw = (ntiles + nwg - 1) / nwg;
+  return (ntiles + *tpw - 1) / *tpw;
+}
+
+template <class T, int C, int O, int TM, int PV>
+static int launch_gather_mfma_pv(const GatherArgs& a, size_t lds, hipStream_t s) {
+  const void* fn = (const void*)gather_mfma_kernel<T, C, O, TM, PV>;
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds(fn, lds, &lds_set, "gather_mfma_kernel");
+  if (rc != VQA_OK) return rc;
+  const int ntm = (a.T_out + TM - 1) / TM;
+  const int ntiles = ntm * a.B;
+  static int per_cu = 0;
+  static size_t per_cu_lds = 0;
+  int tpw = 0;
+  const int nwg = persistent_grid(fn, lds, &per_cu, &per_cu_lds, ntiles, &tpw);
   hipLaunchKernelGGL((gather_mfma_kernel<T, C, O, TM, PV>), dim3(nwg), dim3(256), lds, s, a, ntm, ntiles, tpw);
   VQA_LAUNCHED("gather_mfma_kernel");
   return VQA_OK;
 }
 
+// epilogue tiles staged per tile: ReLU' mask / conv input (fused wgrad), residual
+static int gather_nep(const GatherArgs& a, bool fw) {
+  return (((a.flags & VQA_POST_MASK) || fw) ? 1 : 0) + ((a.flags & VQA_ADD_RESIDUAL) ? 1 : 0);
+}
+
 template <class T, int C, int O, int TM>
 static int launch_gather_mfma_t(const GatherArgs& a, hipStream_t s) {
-  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>(), ES = O + lds_pad<T>();
+  constexpr int XS = C + lds_pad<T>(), WS = C + lds_pad<T>();
   const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
-  const bool pair = a.wmode == W_PAIR;
-  const int nep = ((a.flags & VQA_POST_MASK) ? 1 : 0) + ((a.flags & VQA_ADD_RESIDUAL) ? 1 : 0);
+  const int nep = gather_nep(a, false);
   const size_t ebytes = (size_t)TM * O * sizeof(T);
-  (void)pair;
-  (void)ES;
   const size_t lds = ((size_t)a.K * O * WS + (size_t)rows_in * XS) * sizeof(T) + 2 * ebytes;
   VQA_REQUIRE(lds <= 160 * 1024, VQA_E_UNSUPPORTED, "gather conv: LDS tile too large (%zu B)", lds);
-  // 16-byte chunks per tile held in registers per thread
+  // 16-byte chunks per tile held in registers per thread; a tile only a few chunks over a multiple of
+  // 256 must not pay for the next size up
   const long long chunks = (long long)rows_in * C * sizeof(T) / 16 + (long long)nep * TM * O * sizeof(T) / 16;
   const int pv = (int)((chunks + 255) / 256);
+  if (pv <= 3) return launch_gather_mfma_pv<T, C, O, TM, 3>(a, lds, s);
   if (pv <= 4) return launch_gather_mfma_pv<T, C, O, TM, 4>(a, lds, s);
+  if (pv <= 5) return launch_gather_mfma_pv<T, C, O, TM, 5>(a, lds, s);
   if (pv <= 8) return launch_gather_mfma_pv<T, C, O, TM, 8>(a, lds, s);
   if (pv <= 12) return launch_gather_mfma_pv<T, C, O, TM, 12>(a, lds, s);
   vqa::set_error("gather conv: tile of %lld chunks exceeds the register stager", chunks);
@@ -1094,14 +1387,80 @@ static int launch_gather_mfma(const GatherArgs& a, hipStream_t s) {
   return VQA_E_UNSUPPORTED;
 }
 
+// ---- the 32-channel kernel
+template <class T, int PVX, int NEP, bool FW>
+static int launch_conv32_k(const GatherArgs& a, hipStream_t s, int* nwg_out) {
+  constexpr int ESZ = (int)sizeof(T), XS = 32 + lds_pad<T>(), XROWS = 256 / (32 / (16 / ESZ)) * PVX;
+  const size_t lds = ((size_t)a.K * 32 * XS + (size_t)XROWS * XS) * ESZ + (size_t)NEP * 128 * 32 * ESZ;
+  const void* fn = (const void*)conv32_kernel<T, PVX, NEP, FW>;
+  static size_t lds_set = 0;
+  const int rc = ensure_dyn_lds(fn, lds, &lds_set, "conv32_kernel");
+  if (rc != VQA_OK) return rc;
+  const int ntm = (a.T_out + 127) / 128;
+  const int ntiles = ntm * a.B;
+  static int per_cu = 0;
+  static size_t per_cu_lds = 0;
+  int tpw = 0;
+  const int nwg = persistent_grid(fn, lds, &per_cu, &per_cu_lds, ntiles, &tpw);
+  if (nwg_out) *nwg_out = nwg;
+  hipLaunchKernelGGL((conv32_kernel<T, PVX, NEP, FW>), dim3(nwg), dim3(256), lds, s, a, ntm, ntiles, tpw);
+  VQA_LAUNCHED("conv32_kernel");
+  return VQA_OK;
+}
+
+template <class T, int PVX, bool FW>
+static int launch_conv32_n(const GatherArgs& a, int nep, hipStream_t s, int* nwg_out) {
+  if constexpr (!FW) {
+    if (nep == 0) return launch_conv32_k<T, PVX, 0, FW>(a, s, nwg_out);
+  }
+  if (nep == 1) return launch_conv32_k<T, PVX, 1, FW>(a, s, nwg_out);
+  return launch_conv32_k<T, PVX, 2, FW>(a, s, nwg_out);
+}
+
+// x chunks per thread the 32-channel kernel stages for this launch (0: not applicable)
+static int conv32_pvx(const GatherArgs& a, int dtype, bool fw) {
+  if (a.C != 32 || a.O != 32 || a.wmode == W_PAIR || a.K > 4 || a.S > 2) return 0;
+  if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return 0;
+  if (fw && (a.S != 1 || a.K > 3 || a.wmode != W_FLIP_T)) return 0;
+  const int esz = dtype == VQA_BF16 ? 2 : 4;
+  if ((long long)a.T_in * 32 * esz >= (1ll << 29) || (long long)a.T_out * 32 * esz >= (1ll << 29)) return 0;
+  const int rows_in = 127 * a.S + (a.K - 1) * a.D + 1;
+  const int chunks = rows_in * 32 * esz / 16;
+  const int pv = (chunks + 255) / 256;
+  const int opts_bf16[] = {3, 5}, opts_f32[] = {5, 6, 9};
+  const int* opts = esz == 2 ? opts_bf16 : opts_f32;
+  const int nopt = esz == 2 ? 2 : 3;
+  for (int i = 0; i < nopt; ++i) {
+    if (pv <= opts[i]) {
+      const int xs = 32 + 16 / esz, xrows = 256 / (32 * esz / 16) * opts[i];
+      const size_t lds = ((size_t)a.K * 32 * xs + (size_t)xrows * xs) * esz + 2 * 128 * 32 * esz;
+      return lds <= 150 * 1024 ? opts[i] : 0;
+    }
+  }
+  return 0;
+}
+
+template <class T, bool FW>
+static int launch_conv32(const GatherArgs& a, int pvx, hipStream_t s, int* nwg_out) {
+  const int nep = gather_nep(a, FW);
+  if constexpr (sizeof(T) == 2) {
+    if (pvx == 3) return launch_conv32_n<T, 3, FW>(a, nep, s, nwg_out);
+    return launch_conv32_n<T, 5, FW>(a, nep, s, nwg_out);
+  } else {
+    if (pvx == 5) return launch_conv32_n<T, 5, FW>(a, nep, s, nwg_out);
+    if (pvx == 6) return launch_conv32_n<T, 6, FW>(a, nep, s, nwg_out);
+    return launch_conv32_n<T, 9, FW>(a, nep, s, nwg_out);
+  }
+}
+
 static bool mfma_ok(const GatherArgs& a, int dtype) {
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return false;
   if (!((a.C == 32 || a.C == 64) && (a.O == 32 || a.O == 64 || a.O == 128))) return false;
   const int tm = gather_tm(a.O, a.S);
   const int rows_in = (tm - 1) * a.S + (a.K - 1) * a.D + 1;
-  const int nep = ((a.flags & VQA_POST_MASK) ? 1 : 0) + ((a.flags & VQA_ADD_RESIDUAL) ? 1 : 0);
   const int esz = dtype == VQA_BF16 ? 2 : 4;
-  if ((long long)rows_in * a.C * esz / 16 + (long long)nep * tm * a.O * esz / 16 > 12 * 256) return false;
+  const long long chunks = (long long)rows_in * a.C * esz / 16 + (long long)gather_nep(a, false) * tm * a.O * esz / 16;
+  if (chunks > 12 * 256) return false;
   return (size_t)rows_in * (a.C + 8) * 4 + (size_t)a.K * a.O * (a.C + 8) * 4 <= 150 * 1024;
 }
 
@@ -1158,6 +1517,10 @@ int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
           "non-positive shape");
   VQA_ARG(!(a.flags & VQA_POST_MASK) || a.mask, "VQA_POST_MASK without mask");
   VQA_ARG(!(a.flags & VQA_ADD_RESIDUAL) || a.resid, "VQA_ADD_RESIDUAL without residual");
+  if (const int pvx = conv32_pvx(a, dtype, false)) {
+    return dtype == VQA_BF16 ? launch_conv32<bf16, false>(a, pvx, s, nullptr)
+                             : launch_conv32<float, false>(a, pvx, s, nullptr);
+  }
   if (mfma_ok(a, dtype)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
   const bool xf = dtype == VQA_F32 || (a.flags & VQA_X_F32);
   const bool yf = dtype == VQA_F32 || (a.flags & VQA_Y_F32);
@@ -1459,6 +1822,75 @@ extern "C" int vqa_conv1d_transpose_bwd_weight_partials(const void* x, const voi
   const int f = (swap_xy_flags(flags) & (VQA_X_F32 | VQA_Y_F32)) | WG_DB_FROM_X;
   return run_wgrad(dy, x, dw, db, B, T_out, T_in, C_out, C_in, K, stride, 1, pad_left, f, dtype, workspace, ws_bytes,
                    (hipStream_t)stream, desc);
+}
+
+// ---- fused data + weight gradient of a stride-1 conv whose input u feeds it through an optional ReLU
+static size_t fused_bwd_ws(int C_in, int C_out, int K) {
+  return (size_t)num_cus() * kMaxGatherPerCU * (size_t)(K * C_in * C_out + C_out) * sizeof(float);
+}
+
+static GatherArgs fused_bwd_args(const void* dy, const float* w, const void* x, const void* residual, void* dx, int B,
+                                 int T_in, int T_out, int C_in, int C_out, int K, int dilation, int pad_left,
+                                 int flags) {
+  const bool relu = flags & VQA_PRE_RELU;
+  const int f = swap_xy_flags(flags & (VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32)) | (relu ? VQA_POST_MASK : 0);
+  GatherArgs a{dy, w, nullptr, residual, x, dx, B, T_out, T_in, C_out, C_in, K, 1, dilation,
+               (K - 1) * dilation - pad_left, W_FLIP_T, K, 0, T_in, f};
+  a.wrelu = relu ? 1 : 0;
+  return a;
+}
+
+extern "C" size_t vqa_conv1d_bwd_data_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K,
+                                                       int stride, int dilation, int pad_left, int flags, int dtype) {
+  size_t need = wgrad_ws(dtype, B, T_in, T_out, C_in, C_out, K, stride, dilation,
+                         flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32));
+  if (stride == 1) {
+    const GatherArgs a = fused_bwd_args(nullptr, nullptr, nullptr, nullptr, nullptr, B, T_in, T_out, C_in, C_out, K,
+                                        dilation, pad_left, flags);
+    if (conv32_pvx(a, dtype, true)) need = std::max(need, fused_bwd_ws(C_in, C_out, K));
+  }
+  return need;
+}
+
+extern "C" int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const void* x, const void* residual,
+                                          void* dx, float* dw, float* db, int B, int T_in, int T_out, int C_in,
+                                          int C_out, int K, int stride, int dilation, int pad_left, int flags,
+                                          int dtype, void* workspace, size_t ws_bytes, vqa_partials_desc* desc,
+                                          vqa_stream_t stream) {
+  VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_data_weight: T_out %d != ceil(T_in/stride)", T_out);
+  VQA_ARG(dy && w && x && dx && dw, "conv1d_bwd_data_weight: null tensor pointer");
+  VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
+  const hipStream_t s = (hipStream_t)stream;
+  if (stride == 1) {
+    GatherArgs a = fused_bwd_args(dy, w, x, residual, dx, B, T_in, T_out, C_in, C_out, K, dilation, pad_left, flags);
+    if (const int pvx = conv32_pvx(a, dtype, true)) {
+      const size_t need = fused_bwd_ws(C_in, C_out, K);
+      VQA_ARG(workspace && ws_bytes >= need, "workspace too small: need %zu bytes, got %zu", need, ws_bytes);
+      a.wpart = (float*)workspace;
+      int nwg = 0;
+      const int rc = dtype == VQA_BF16 ? launch_conv32<bf16, true>(a, pvx, s, &nwg)
+                                       : launch_conv32<float, true>(a, pvx, s, &nwg);
+      if (rc != VQA_OK) return rc;
+      const int KCO = K * C_in * C_out, E = KCO + C_out;
+      if (desc) {
+        *desc = vqa_partials_desc{(const float*)workspace, dw, db, nwg, E, KCO, 0};
+        return VQA_OK;
+      }
+      hipLaunchKernelGGL(reduce_partials_kernel, dim3((E + 63) / 64), dim3(256), 0, s, (const float*)workspace, nwg, E,
+                         KCO, dw, db);
+      VQA_LAUNCHED("reduce_partials_kernel");
+      return VQA_OK;
+    }
+  }
+  // not fusable here: data gradient, then the weight gradient from the same operands
+  const bool relu = flags & VQA_PRE_RELU;
+  int rc = vqa_conv1d_bwd_data(dy, w, relu ? x : nullptr, residual, dx, B, T_in, T_out, C_in, C_out, K, stride,
+                               dilation, pad_left,
+                               (relu ? VQA_POST_MASK : 0) | (flags & (VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32)),
+                               dtype, stream);
+  if (rc != VQA_OK) return rc;
+  return run_wgrad(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
+                   flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, s, desc);
 }
 
 extern "C" int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vqa_stream_t stream) {

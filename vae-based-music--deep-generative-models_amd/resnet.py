@@ -4,7 +4,8 @@ resnet.py:7-29   ResnetConv1DBlock: y = x + Conv1D_k3,d1(ReLU(Conv1D_k3,dil(ReLU
 resnet.py:40-59  DilatedResnet1D: `depth` blocks, dilation dilation_factor**d (or **(d % dilation_cycle)),
                  reversed for decoders.
 Both convs run on the HIP gather-conv kernel with the ReLUs fused into the LDS staging of the input and
-the residual add fused into the epilogue; the backward fuses ReLU' masks and the residual gradient.
+the residual add fused into the epilogue; the backward of each conv is one kernel (data gradient with the
+ReLU' mask and residual gradient fused, plus the weight gradient from the same staged tiles).
 """
 from __future__ import annotations
 
@@ -35,12 +36,10 @@ class ResnetConv1DBlock(Layer):
     def backward(self, dy):
         x, h = self._saved
         self._saved = None
-        T = x.shape[1]
-        dh = self.conv_b.backward_data(dy, T, self.cdt, mask=h)
-        self.conv_b.backward_weight(h, dy, self.cdt, pre_relu=True)
-        dx = self.conv_a.backward_data(dh, T, self.cdt, mask=x, residual=dy)
-        self.conv_a.backward_weight(x, dh, self.cdt, pre_relu=True)
-        return dx
+        # each conv's data- and weight-gradient in one kernel: its input (h, x) is both the ReLU' mask and
+        # the weight-gradient operand, so it is read once
+        dh = self.conv_b.backward_data_weight(dy, h, self.cdt, pre_relu=True)
+        return self.conv_a.backward_data_weight(dh, x, self.cdt, pre_relu=True, residual=dy)
 
 
 class DilatedResnet1D(Layer):

@@ -160,6 +160,18 @@ class Conv1D:
             V.conv1d_bwd_weight(*args)
 
 
+    def backward_data_weight(self, dy, x, cdt, pre_relu=False, residual=None):
+        """backward_data (ReLU' mask = the conv input x when pre_relu) and backward_weight in one pass."""
+        B, T, _ = x.shape
+        dx = torch.empty((B, T, self.cin), dtype=cdt, device=dy.device)
+        fl = _flags_for(x, dy.dtype, cdt) | (V.PRE_RELU if pre_relu else 0) | \
+            (V.ADD_RESIDUAL if residual is not None else 0)
+        V.conv1d_bwd_data_weight(dy, self.w, x, residual, dx, self.store.grad_view(f"{self.name}/kernel"),
+                                 self.store.grad_view(f"{self.name}/bias"), B, T, dy.shape[1], self.cin, self.cout,
+                                 self.K, self.s, self.d, self.pad(T), fl, V.dtype_code(cdt), self.store.deferred)
+        return dx
+
+
 class Conv1DTranspose:
     """keras layers.Conv1DTranspose(filters, 2*stride, strides=stride, padding='same') — kernel
     (K, C_out, C_in), bias (C_out). Replaces the TF op at encdec.py:67-68."""

@@ -27,6 +27,7 @@ EXPORTED = [
     "vqa_vq_reset_rows", "vqa_vq_ema_apply", "vqa_reset_perm_index",
     "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_counter_add",
     "vqa_conv1d_bwd_weight_partials", "vqa_conv1d_transpose_bwd_weight_partials", "vqa_reduce_partials",
+    "vqa_conv1d_bwd_data_weight", "vqa_conv1d_bwd_data_weight_workspace",
 ]
 
 
@@ -73,6 +74,8 @@ _SIGS = {
     "vqa_conv1d_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
     "vqa_conv1d_transpose_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONVT + [_P, _S, _P, _P]),
     "vqa_reduce_partials": (_I, [_P, _I, _P]),
+    "vqa_conv1d_bwd_data_weight": (_I, [_P, _P, _P, _P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
+    "vqa_conv1d_bwd_data_weight_workspace": (_S, _CONV),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -187,6 +190,22 @@ def conv1d_bwd_weight_deferred(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, st
                                                 stride, dilation, pad, flags, dtype, ptr(ws), ws.numel(),
                                                 ctypes.byref(d), stream()), "vqa_conv1d_bwd_weight_partials")
     deferred.add(d, ws)
+
+
+def conv1d_bwd_data_weight(dy, w, x, residual, dx, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad,
+                           flags, dtype, deferred=None):
+    """dx and (dw, db) of one Conv1D in one pass (vqa_conv1d_bwd_data_weight); `x` is the conv input (its
+    ReLU' mask with VQA_PRE_RELU). With `deferred` the weight-gradient reduction joins its batch."""
+    n = lib().vqa_conv1d_bwd_data_weight_workspace(B, T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags,
+                                                    dtype)
+    ws = workspace(n, x.device)
+    d = PartialsDesc() if deferred is not None else None
+    _check(lib().vqa_conv1d_bwd_data_weight(ptr(dy), ptr(w), ptr(x), ptr(residual), ptr(dx), ptr(dw), ptr(db), B,
+                                            T_in, T_out, C_in, C_out, K, stride, dilation, pad, flags, dtype,
+                                            ptr(ws), ws.numel(), ctypes.byref(d) if d is not None else None,
+                                            stream()), "vqa_conv1d_bwd_data_weight")
+    if deferred is not None:
+        deferred.add(d, ws)
 
 
 def conv1d_transpose_bwd_weight_deferred(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype,
