@@ -175,6 +175,23 @@ int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, cons
 /* *counter += delta on the stream (graph-capturable step counters). */
 int vqa_counter_add(int64_t* counter, int64_t delta, vqa_stream_t stream);
 
+/* ---- multi-resolution spectral loss --------------------------------------------------------------
+ * Replaces vqvae.py:309-326 (_multispectral_loss) over data_utils.py:25-30 (spectral = |tf.signal.stft|)
+ * and data_utils.py:33-40 (norm = tf.norm 'fro'), plus its GradientTape backward (vqvae.py:143):
+ *   loss_out[0] = mean_b mean_res ||S_x[b] - S_r[b]||_F / ||S_x[b]||_F,
+ *   S = |rfft(frame * hann_periodic(win), n_fft)|, frame f = sig[f*hop : f*hop + win], F = 1 + (T-win)/hop
+ *   (no centering, pad_end=False), dr = d loss_out / d r (nullable: loss only; abs'(0) = 0 as in TF),
+ *   item_loss[b] = mean_res of item b's loss (nullable).
+ * x, r, dr: (B, T) fp32. STFT parameters are host arrays of nres (<= 8) entries; n_fft in {256, 512, 1024,
+ * 2048}, win <= n_fft, win <= T. with_grad selects the workspace size with (1) or without (0) dr. */
+int vqa_spectral_loss(const float* x, const float* r, float* loss_out, float* dr, float* item_loss, int B, int T,
+                      const int* n_fft, const int* hop, const int* win, int nres, void* workspace, size_t ws_bytes,
+                      vqa_stream_t stream);
+size_t vqa_spectral_loss_workspace(int B, int T, const int* n_fft, const int* hop, const int* win, int nres,
+                                   int with_grad);
+/* data_utils.py:25-30 spectral(x) for one resolution: mag (B, F, n_fft/2 + 1) fp32 = |tf.signal.stft(x)|. */
+int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int n_fft, int hop, int win, vqa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,27 @@
+"""Per-step kernel breakdown from a rocprofv3 kernel_trace.csv (GPU dev tool): takes the interval between two
+consecutive adam_kernel dispatches (one train step) in the middle of the run and groups kernel time.
+
+    python tools/step_breakdown.py KERNEL_TRACE_CSV [STEP_INDEX]
+"""
+import collections
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+adam = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else len(adam) // 2
+a, b = adam[k], adam[k + 1]
+step = rows[a + 1:b + 1]
+wall = (int(step[-1]["End_Timestamp"]) - int(step[0]["Start_Timestamp"])) / 1e6
+busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step) / 1e6
+print(f"step {k}: {len(step)} dispatches, wall {wall:.3f} ms, kernel-busy {busy:.3f} ms")
+by = collections.defaultdict(lambda: [0, 0.0])
+for r in step:
+    n = r["Kernel_Name"]
+    key = n.split("(")[0][:90] + f"  grid={r['Grid_Size_X']}"
+    if len(sys.argv) > 3:
+        key = n[:100]
+    by[key][0] += 1
+    by[key][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+for key, (c, t) in sorted(by.items(), key=lambda kv: -kv[1][1])[:60]:
+    print(f"{t:8.3f} ms {c:5d}x  {key}")

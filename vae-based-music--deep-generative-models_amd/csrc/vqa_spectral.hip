@@ -1,0 +1,373 @@
+// vqa_spectral.hip — multi-resolution spectral loss and its gradient (gfx950).
+//
+// Replaces the reference's per-level
+//   data_utils.py:25-30  spectral(x) = |tf.signal.stft(x, frame_length=win, frame_step=hop, fft_length=n_fft)|
+//   data_utils.py:33-40  norm(x)     = tf.norm(x, 'fro', axis=[-2, -1])
+//   vqvae.py:309-326     _multispectral_loss = mean_b mean_res norm(S_x - S_r) / norm(S_x)
+// and the GradientTape backward of that expression w.r.t. the reconstruction (vqvae.py:143).
+//
+// One workgroup owns one STFT frame at a time (persistent loop over frames): the windowed target and
+// reconstruction frames are transformed by an in-LDS radix-4 Stockham FFT (fp32, twiddles from fp64
+// sincospi), the per-bin magnitudes |X_k|, |R_k| give the frame's partial sums sum (|X|-|R|)^2 and sum |X|^2,
+// and — for the gradient — the bin gradient G_k = (|R_k| - |X_k|) R_k / |R_k| (0 where |R_k| = 0, TF's
+// abs'(0)) is mapped back to the time domain by the adjoint of the one-sided rfft (an inverse FFT of the
+// Hermitian extension of G), windowed, and written unscaled per frame. The per-item scale
+// 1 / (nres * B * ||S_x - S_r|| * ||S_x||) is known only after every frame of the item is done, so a second
+// kernel reduces the partial sums per (item, resolution) and a third overlap-adds the frame gradients
+// (fixed summation order: deterministic) and applies the scales. No atomics, no host sync, graph-capturable.
+#include "vqa_common.h"
+
+namespace vqa {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 cmul(f32x2 a, f32x2 b) {
+  return f32x2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ f32x2 conj2(f32x2 a) { return f32x2{a.x, -a.y}; }
+__device__ __forceinline__ float cabs2(f32x2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+
+// One radix-4 Stockham stage at stride S of an N-point transform: x -> y. tw[k] = exp(-2 pi i k / N).
+template <int N, int S, bool INV>
+__device__ __forceinline__ void fft_stage4(const f32x2* x, f32x2* y, const f32x2* tw) {
+  constexpr int n = N / S, m = n / 4;
+  for (int j = threadIdx.x; j < N / 4; j += 256) {
+    const int p = j / S, q = j % S;
+    const f32x2 a0 = x[q + S * p], a1 = x[q + S * (p + m)], a2 = x[q + S * (p + 2 * m)], a3 = x[q + S * (p + 3 * m)];
+    f32x2 w1 = tw[p * S], w2 = tw[2 * p * S], w3 = tw[3 * p * S];
+    if (INV) {
+      w1 = conj2(w1);
+      w2 = conj2(w2);
+      w3 = conj2(w3);
+    }
+    const f32x2 b0 = a0 + a2, b1 = a0 - a2, b2 = a1 + a3, d = a1 - a3;
+    const f32x2 jd = INV ? f32x2{-d.y, d.x} : f32x2{d.y, -d.x};  // +i d (inverse) / -i d (forward)
+    y[q + S * (4 * p)] = b0 + b2;
+    y[q + S * (4 * p + 1)] = cmul(b1 + jd, w1);
+    y[q + S * (4 * p + 2)] = cmul(b0 - b2, w2);
+    y[q + S * (4 * p + 3)] = cmul(b1 - jd, w3);
+  }
+}
+
+// the last stage when log2(N) is odd: n = 2, S = N/2
+template <int N>
+__device__ __forceinline__ void fft_stage2(const f32x2* x, f32x2* y) {
+  for (int q = threadIdx.x; q < N / 2; q += 256) {
+    const f32x2 a = x[q], b = x[q + N / 2];
+    y[q] = a + b;
+    y[q + N / 2] = a - b;
+  }
+}
+
+template <int N, int S, bool INV>
+__device__ __forceinline__ void fft_rec(f32x2* x, f32x2* y, const f32x2* tw) {
+  constexpr int n = N / S;
+  if constexpr (n >= 4) {
+    fft_stage4<N, S, INV>(x, y, tw);
+    __syncthreads();
+    fft_rec<N, S * 4, INV>(y, x, tw);
+  } else if constexpr (n == 2) {
+    fft_stage2<N>(x, y);
+    __syncthreads();
+  }
+}
+
+template <int N> constexpr int fft_stages() {
+  int s = 0, n = N;
+  while (n >= 4) {
+    n /= 4;
+    ++s;
+  }
+  return s + (n == 2 ? 1 : 0);
+}
+
+// In-place (logically) N-point FFT of a[] in LDS; b[] is scratch. Returns the buffer holding the result
+// (natural order). Unnormalised in both directions. Caller syncs before (a written) — ends with a sync.
+template <int N, bool INV>
+__device__ __forceinline__ f32x2* fft(f32x2* a, f32x2* b, const f32x2* tw) {
+  fft_rec<N, 1, INV>(a, b, tw);
+  return (fft_stages<N>() & 1) ? b : a;
+}
+
+enum { SPEC_GRAD = 0, SPEC_LOSS = 1, SPEC_MAG = 2 };
+
+struct SpecFrameArgs {
+  const float* x;  // target (B, T) fp32
+  const float* r;  // reconstruction (B, T) fp32 (unused for SPEC_MAG)
+  float* fg;       // SPEC_GRAD: unscaled frame gradients (B*F, win)
+  float* part;     // SPEC_GRAD/LOSS: per-frame (sum (|X|-|R|)^2, sum |X|^2)
+  float* mag;      // SPEC_MAG: |X| (B*F, N/2+1)
+  int B, T, F, hop, win;
+};
+
+template <int N, int MODE>
+__global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  f32x2* buf0 = (f32x2*)smem;
+  f32x2* buf1 = buf0 + N;
+  f32x2* tw = buf1 + N;
+  float* wn = (float*)(tw + N);
+  constexpr int KB = N / 2 + 1, NB = (KB + 255) / 256;
+  const int tid = threadIdx.x;
+
+  // twiddles exp(-2 pi i k / N) and the periodic Hann window (tf.signal.hann_window(win, periodic=True)),
+  // both evaluated in fp64 and rounded once
+  for (int k = tid; k < N; k += 256) {
+    double s, c;
+    sincospi(2.0 * (double)k / (double)N, &s, &c);
+    tw[k] = f32x2{(float)c, (float)-s};
+  }
+  for (int n = tid; n < a.win; n += 256) wn[n] = (float)(0.5 - 0.5 * cospi(2.0 * (double)n / (double)a.win));
+  __syncthreads();
+
+  __shared__ float red[4];
+  const int nframes = a.B * a.F;
+  for (int fi = blockIdx.x; fi < nframes; fi += gridDim.x) {
+    const int bb = fi / a.F, f = fi - bb * a.F;
+    const size_t off = (size_t)bb * a.T + (size_t)f * a.hop;
+    const float* xs = a.x + off;
+    for (int n = tid; n < N; n += 256) buf0[n] = n < a.win ? f32x2{xs[n] * wn[n], 0.f} : f32x2{0.f, 0.f};
+    __syncthreads();
+    const f32x2* X = fft<N, false>(buf0, buf1, tw);
+    float mx[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int k = tid + 256 * j;
+      mx[j] = k < KB ? cabs2(X[k]) : 0.f;
+    }
+    if constexpr (MODE == SPEC_MAG) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int k = tid + 256 * j;
+        if (k < KB) a.mag[(size_t)fi * KB + k] = mx[j];
+      }
+      __syncthreads();
+      continue;
+    } else {
+      __syncthreads();  // every read of X done before buf0/buf1 are reused
+      const float* rs = a.r + off;
+      for (int n = tid; n < N; n += 256) buf0[n] = n < a.win ? f32x2{rs[n] * wn[n], 0.f} : f32x2{0.f, 0.f};
+      __syncthreads();
+      f32x2* R = fft<N, false>(buf0, buf1, tw);
+      f32x2* H = (R == buf0) ? buf1 : buf0;  // free since the last FFT stage's sync
+      float sd = 0.f, sx = 0.f;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int k = tid + 256 * j;
+        if (k < KB) {
+          const f32x2 rk = R[k];
+          const float mr = cabs2(rk), d = mx[j] - mr;
+          sd += d * d;
+          sx += mx[j] * mx[j];
+          if constexpr (MODE == SPEC_GRAD) {
+            // dL/d(Re,Im)R_k = (|R|-|X|) R/|R|; Hermitian extension for the adjoint of the one-sided rfft
+            const float g = mr > 0.f ? (mr - mx[j]) / mr : 0.f;
+            const f32x2 G = f32x2{g * rk.x, g * rk.y};
+            if (k == 0 || k == N / 2) {
+              H[k] = f32x2{G.x, 0.f};
+            } else {
+              H[k] = f32x2{0.5f * G.x, 0.5f * G.y};
+              H[N - k] = f32x2{0.5f * G.x, -0.5f * G.y};
+            }
+          }
+        }
+      }
+      sd = block_sum_256(sd, red);
+      __syncthreads();
+      sx = block_sum_256(sx, red);
+      if (tid == 0) {
+        a.part[2 * (size_t)fi] = sd;
+        a.part[2 * (size_t)fi + 1] = sx;
+      }
+      if constexpr (MODE == SPEC_GRAD) {
+        // block_sum_256's syncs ordered the H writes before this point
+        f32x2* other = (H == buf0) ? buf1 : buf0;
+        const f32x2* Y = fft<N, true>(H, other, tw);
+        float* out = a.fg + (size_t)fi * a.win;
+        for (int n = tid; n < a.win; n += 256) out[n] = Y[n].x * wn[n];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+constexpr int SPEC_MAX_RES = 8;
+
+struct SpecScaleArgs {
+  const float* part[SPEC_MAX_RES];
+  int F[SPEC_MAX_RES];
+  float* lossbr;  // (B, nres) per item and resolution: ||S_x - S_r|| / ||S_x||
+  float* scale;   // (B, nres): inv / (||S_x - S_r|| * ||S_x||)
+  int nres;
+  float inv;  // 1 / (nres * B)
+};
+
+__global__ __launch_bounds__(256) void spec_scale_kernel(SpecScaleArgs a) {
+  __shared__ float red[4];
+  const int b = blockIdx.x / a.nres, res = blockIdx.x - b * a.nres;
+  const int F = a.F[res];
+  const float* p = a.part[res] + (size_t)b * F * 2;
+  float sd = 0.f, sx = 0.f;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    sd += p[2 * f];
+    sx += p[2 * f + 1];
+  }
+  sd = block_sum_256(sd, red);
+  __syncthreads();
+  sx = block_sum_256(sx, red);
+  if (threadIdx.x == 0) {
+    const float nd = sqrtf(sd), nx = sqrtf(sx);
+    a.lossbr[blockIdx.x] = nd / nx;
+    a.scale[blockIdx.x] = a.inv / (nd * nx);
+  }
+}
+
+struct SpecGatherArgs {
+  const float* fg[SPEC_MAX_RES];
+  int F[SPEC_MAX_RES], hop[SPEC_MAX_RES], win[SPEC_MAX_RES];
+  const float* lossbr;
+  const float* scale;
+  float* dr;         // (B, T) or null (loss only)
+  float* loss_out;   // [1]: mean_b mean_res lossbr
+  float* item_loss;  // (B) or null: mean_res lossbr
+  int B, T, nres;
+};
+
+__global__ __launch_bounds__(256) void spec_gather_kernel(SpecGatherArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int b = 0; b < a.B; ++b) {
+      float s = 0.f;
+      for (int r = 0; r < a.nres; ++r) s += a.lossbr[b * a.nres + r];
+      s = s / (float)a.nres;
+      if (a.item_loss) a.item_loss[b] = s;
+      tot += s;
+    }
+    a.loss_out[0] = tot / (float)a.B;
+  }
+  if (!a.dr) return;
+  const long long n = (long long)a.B * a.T;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int b = (int)(i / a.T), t = (int)(i - (long long)b * a.T);
+    float acc = 0.f;
+    for (int r = 0; r < a.nres; ++r) {
+      const int hop = a.hop[r], win = a.win[r], F = a.F[r];
+      const int f_hi = min(F - 1, t / hop);
+      const int f_lo = t >= win ? (t - win) / hop + 1 : 0;
+      const float* g = a.fg[r] + (size_t)b * F * win;
+      float s = 0.f;
+      for (int f = f_lo; f <= f_hi; ++f) s += g[(size_t)f * win + (t - f * hop)];
+      acc += a.scale[b * a.nres + r] * s;
+    }
+    a.dr[i] = acc;
+  }
+}
+
+template <int N, int MODE>
+static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
+  const size_t lds = (size_t)3 * N * sizeof(f32x2) + (size_t)fa.win * sizeof(float);
+  const int nframes = fa.B * fa.F;
+  const int grid = nframes < 4096 ? nframes : 4096;
+  hipLaunchKernelGGL((spec_frame_kernel<N, MODE>), dim3(grid), dim3(256), lds, s, fa);
+  VQA_LAUNCHED("spec_frame_kernel");
+  return VQA_OK;
+}
+
+template <int MODE>
+static int dispatch_frames(int n_fft, const SpecFrameArgs& fa, hipStream_t s) {
+  switch (n_fft) {
+    case 256: return launch_frames<256, MODE>(fa, s);
+    case 512: return launch_frames<512, MODE>(fa, s);
+    case 1024: return launch_frames<1024, MODE>(fa, s);
+    case 2048: return launch_frames<2048, MODE>(fa, s);
+    default: set_error("spectral: n_fft %d unsupported (256, 512, 1024, 2048)", n_fft); return VQA_E_UNSUPPORTED;
+  }
+}
+
+static size_t align64(size_t n) { return (n + 63) & ~(size_t)63; }
+
+// workspace layout (floats): per resolution [fg (grad only) | part], then [lossbr | scale]
+static int spec_layout(int B, int T, const int* n_fft, const int* hop, const int* win, int nres, bool grad,
+                       size_t* fg_off, size_t* part_off, int* F, size_t* tail_off, size_t* total) {
+  if (B <= 0 || T <= 0 || nres <= 0 || nres > SPEC_MAX_RES || !n_fft || !hop || !win) return VQA_E_INVALID_ARG;
+  size_t o = 0;
+  for (int r = 0; r < nres; ++r) {
+    if (hop[r] <= 0 || win[r] <= 0 || win[r] > n_fft[r] || win[r] > T) return VQA_E_INVALID_ARG;
+    F[r] = 1 + (T - win[r]) / hop[r];
+    fg_off[r] = o;
+    if (grad) o += align64((size_t)B * F[r] * win[r]);
+    part_off[r] = o;
+    o += align64((size_t)B * F[r] * 2);
+  }
+  *tail_off = o;
+  o += align64((size_t)B * nres * 2);
+  *total = o * sizeof(float);
+  return VQA_OK;
+}
+
+}  // namespace vqa
+
+using namespace vqa;
+
+extern "C" size_t vqa_spectral_loss_workspace(int B, int T, const int* n_fft, const int* hop, const int* win,
+                                              int nres, int with_grad) {
+  size_t fo[SPEC_MAX_RES], po[SPEC_MAX_RES], tail, total;
+  int F[SPEC_MAX_RES];
+  if (spec_layout(B, T, n_fft, hop, win, nres, with_grad != 0, fo, po, F, &tail, &total) != VQA_OK) return 0;
+  return total;
+}
+
+extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out, float* dr, float* item_loss, int B,
+                                 int T, const int* n_fft, const int* hop, const int* win, int nres, void* workspace,
+                                 size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(x && r && loss_out, "spectral_loss: null pointer");
+  const bool grad = dr != nullptr;
+  size_t fo[SPEC_MAX_RES], po[SPEC_MAX_RES], tail, total;
+  int F[SPEC_MAX_RES];
+  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, grad, fo, po, F, &tail, &total) == VQA_OK,
+          "spectral_loss: bad shape (B=%d T=%d nres=%d; need 0 < win <= n_fft, win <= T, hop > 0)", B, T, nres);
+  VQA_ARG(workspace && ws_bytes >= total, "spectral_loss: workspace %zu < %zu bytes", ws_bytes, total);
+  hipStream_t s = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  SpecScaleArgs sa{};
+  SpecGatherArgs ga{};
+  for (int i = 0; i < nres; ++i) {
+    SpecFrameArgs fa{x, r, ws + fo[i], ws + po[i], nullptr, B, T, F[i], hop[i], win[i]};
+    const int rc = grad ? dispatch_frames<SPEC_GRAD>(n_fft[i], fa, s) : dispatch_frames<SPEC_LOSS>(n_fft[i], fa, s);
+    if (rc != VQA_OK) return rc;
+    sa.part[i] = ws + po[i];
+    sa.F[i] = F[i];
+    ga.fg[i] = ws + fo[i];
+    ga.F[i] = F[i];
+    ga.hop[i] = hop[i];
+    ga.win[i] = win[i];
+  }
+  sa.lossbr = ws + tail;
+  sa.scale = ws + tail + (size_t)B * nres;
+  sa.nres = nres;
+  sa.inv = (float)(1.0 / ((double)nres * (double)B));
+  hipLaunchKernelGGL(spec_scale_kernel, dim3(B * nres), dim3(256), 0, s, sa);
+  VQA_LAUNCHED("spec_scale_kernel");
+  ga.lossbr = sa.lossbr;
+  ga.scale = sa.scale;
+  ga.dr = dr;
+  ga.loss_out = loss_out;
+  ga.item_loss = item_loss;
+  ga.B = B;
+  ga.T = T;
+  ga.nres = nres;
+  long long nb = grad ? ((long long)B * T + 255) / 256 : 1;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(spec_gather_kernel, dim3((int)nb), dim3(256), 0, s, ga);
+  VQA_LAUNCHED("spec_gather_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int n_fft, int hop, int win,
+                                  vqa_stream_t stream) {
+  VQA_ARG(x && mag && B > 0 && hop > 0 && win > 0 && win <= n_fft && win <= T,
+          "stft_magnitude: bad arguments (B=%d T=%d n_fft=%d hop=%d win=%d)", B, T, n_fft, hop, win);
+  const int F = 1 + (T - win) / hop;
+  SpecFrameArgs fa{x, nullptr, nullptr, nullptr, mag, B, T, F, hop, win};
+  return dispatch_frames<SPEC_MAG>(n_fft, fa, (hipStream_t)stream);
+}

@@ -4,67 +4,69 @@ data_utils.py:19-22  STFT_ARGS (n_fft, hop_length, window_size) per resolution
 data_utils.py:25-30  spectral = |tf.signal.stft(x, frame_length=win, frame_step=hop, fft_length=n_fft)|
 data_utils.py:33-40  norm = tf.norm(x, 'fro', axis=[-2, -1])
 vqvae.py:309-326     _multispectral_loss = mean_res ||S_x - S_r||_F / ||S_x||_F
-The STFT runs on hipFFT (torch.fft) with TF framing: no centering, frame t = x[t*hop : t*hop+win] times
-a periodic Hann window, rfft zero-padded at the end to n_fft. The target spectrogram is computed once
-per step and shared by all levels (the reference recomputes the same values per level).
+The STFT, the loss and its gradient run in libvqa's spectral kernels (csrc/vqa_spectral.hip: in-LDS radix-4
+FFTs with TF framing — no centering, frame t = x[t*hop : t*hop+win] times a periodic Hann window, rfft
+zero-padded at the end to n_fft).
 
 File decoding (librosa / GTZAN, data_utils.py:43-206) is out of scope: the north star trains on
 synthetic chunks; `synthetic_batch` generates them.
 """
 from __future__ import annotations
 
-import math
-from typing import List, Tuple
-
 import numpy as np
 import torch
+
+import vqa_lib as V
 
 STFT_ARGS = [(2048, 1024, 512),  # n_fft
              (240, 120, 50),  # hop_length
              (1200, 600, 240)]  # window_size
 
-_WINDOWS = {}
-
-
-def _hann(win: int, device) -> torch.Tensor:
-    key = (win, str(device))
-    if key not in _WINDOWS:
-        k = torch.arange(win, dtype=torch.float64)
-        _WINDOWS[key] = (0.5 - 0.5 * torch.cos(2 * math.pi * k / win)).to(torch.float32).to(device)
-    return _WINDOWS[key]
-
 
 def spectral(x: torch.Tensor, n_fft: int, hop_length: int, window_length: int) -> torch.Tensor:
-    frames = x.unfold(-1, window_length, hop_length)
-    return torch.fft.rfft(frames * _hann(window_length, x.device), n=n_fft).abs()
+    """data_utils.py:25-30 |tf.signal.stft(x, window_length, hop_length, n_fft)| on the HIP FFT kernel:
+    x (..., T) fp32 device tensor -> (..., F, n_fft//2 + 1) fp32."""
+    lead, T = tuple(x.shape[:-1]), x.shape[-1]
+    xf = x.detach().reshape(-1, T).float().contiguous()
+    if window_length > T:
+        raise ValueError(f"spectral: signal of {T} samples is shorter than the {window_length}-sample window")
+    F = 1 + (T - window_length) // hop_length
+    mag = torch.empty(xf.shape[0], F, n_fft // 2 + 1, dtype=torch.float32, device=x.device)
+    V.stft_magnitude(xf, mag, n_fft, hop_length, window_length)
+    return mag.reshape(*lead, F, n_fft // 2 + 1)
 
 
 def norm(x: torch.Tensor) -> torch.Tensor:
+    """data_utils.py:33-40 tf.norm(x, 'fro', axis=[-2, -1])."""
     return torch.sqrt((x * x).sum(dim=(-2, -1)))
 
 
 class SpectralTarget:
-    """|S_x| and ||S_x||_F for the three resolutions of one batch (B, T, 1) fp32."""
+    """The target waveform of one batch, (B, T) fp32 on the device. The spectral kernel re-derives |S_x| per
+    frame in LDS next to |S_r| (cheaper than storing and re-reading the target spectrogram per level)."""
 
     def __init__(self, x: torch.Tensor):
-        t = x.reshape(x.shape[0], -1).float()
-        self.specs: List[Tuple[torch.Tensor, torch.Tensor]] = []
-        with torch.no_grad():
-            for n_fft, hop, win in zip(*STFT_ARGS):
-                s = spectral(t, n_fft, hop, win)
-                self.specs.append((s, norm(s)))
+        self.x = x.reshape(x.shape[0], -1).float().contiguous()
+        self.B, self.T = self.x.shape
+        self._ws = {}
+
+    def workspace(self, grad: bool) -> torch.Tensor:
+        if grad not in self._ws:
+            n = V.spectral_loss_workspace(self.B, self.T, *STFT_ARGS, with_grad=grad)
+            self._ws[grad] = V.workspace(n, self.x.device)
+        return self._ws[grad]
 
 
-def multispectral_loss_and_grad(target: SpectralTarget, recon: torch.Tensor):
-    """Returns (mean over batch of the per-item multispectral loss, d loss / d recon (B, T, 1) fp32)."""
-    r = recon.detach().reshape(recon.shape[0], -1).float().requires_grad_(True)
-    with torch.enable_grad():
-        losses = []
-        for (s_x, n_x), (n_fft, hop, win) in zip(target.specs, zip(*STFT_ARGS)):
-            losses.append(norm(s_x - spectral(r, n_fft, hop, win)) / n_x)
-        loss = torch.stack(losses, dim=-1).mean(dim=-1).mean()
-        (g,) = torch.autograd.grad(loss, r)
-    return loss.detach(), g.reshape(recon.shape)
+def multispectral_loss_and_grad(target: SpectralTarget, recon: torch.Tensor, loss_out=None, need_grad=True):
+    """vqvae.py:309-326 _multispectral_loss (mean over the batch of the per-item mean over resolutions) and
+    its gradient d loss / d recon, (B, T, 1) fp32 — one vqa_spectral_loss call. Returns (loss (1,), grad)."""
+    r = recon.reshape(recon.shape[0], -1)
+    if r.dtype != torch.float32:
+        raise ValueError("the multispectral loss takes the fp32 reconstruction")
+    loss = loss_out if loss_out is not None else torch.empty(1, dtype=torch.float32, device=r.device)
+    dr = torch.empty_like(r) if need_grad else None
+    V.spectral_loss(target.x, r.contiguous(), loss, dr, None, *STFT_ARGS, ws=target.workspace(need_grad))
+    return loss, (dr.reshape(recon.shape) if need_grad else None)
 
 
 def synthetic_batch(B: int, T: int, sr: int = 44100, seed: int = 1234) -> np.ndarray:

@@ -28,6 +28,7 @@ EXPORTED = [
     "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_counter_add",
     "vqa_conv1d_bwd_weight_partials", "vqa_conv1d_transpose_bwd_weight_partials", "vqa_reduce_partials",
     "vqa_conv1d_bwd_data_weight", "vqa_conv1d_bwd_data_weight_workspace",
+    "vqa_spectral_loss", "vqa_spectral_loss_workspace", "vqa_stft_magnitude",
 ]
 
 
@@ -76,6 +77,9 @@ _SIGS = {
     "vqa_reduce_partials": (_I, [_P, _I, _P]),
     "vqa_conv1d_bwd_data_weight": (_I, [_P, _P, _P, _P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
     "vqa_conv1d_bwd_data_weight_workspace": (_S, _CONV),
+    "vqa_spectral_loss": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _S, _P]),
+    "vqa_spectral_loss_workspace": (_S, [_I, _I, _P, _P, _P, _I, _I]),
+    "vqa_stft_magnitude": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -293,3 +297,31 @@ def adam_keras(w, g, m, v, step, lr, beta1, beta2, eps, grad_scale):
 
 def counter_add(counter, delta=1):
     _check(lib().vqa_counter_add(ptr(counter), delta, stream()), "vqa_counter_add")
+
+
+def _int_array(vals):
+    return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
+
+
+def spectral_loss_workspace(B, T, n_fft, hop, win, with_grad=True) -> int:
+    n = lib().vqa_spectral_loss_workspace(B, T, _int_array(n_fft), _int_array(hop), _int_array(win), len(n_fft),
+                                          1 if with_grad else 0)
+    if n == 0:
+        raise VQAError(f"spectral_loss: bad shape B={B} T={T} n_fft={n_fft} hop={hop} win={win}")
+    return n
+
+
+def spectral_loss(x, r, loss_out, dr, item_loss, n_fft, hop, win, ws=None):
+    """x, r, dr: (B, T) fp32 device tensors; loss_out: 1-element fp32. dr / item_loss may be None."""
+    B, T = x.shape[0], x.numel() // x.shape[0]
+    nres = len(n_fft)
+    if ws is None:
+        ws = workspace(spectral_loss_workspace(B, T, n_fft, hop, win, dr is not None), x.device)
+    _check(lib().vqa_spectral_loss(ptr(x), ptr(r), ptr(loss_out), ptr(dr), ptr(item_loss), B, T, _int_array(n_fft),
+                                   _int_array(hop), _int_array(win), nres, ptr(ws), ws.numel(), stream()),
+           "vqa_spectral_loss")
+
+
+def stft_magnitude(x, mag, n_fft, hop, win):
+    B, T = x.shape[0], x.numel() // x.shape[0]
+    _check(lib().vqa_stft_magnitude(ptr(x), ptr(mag), B, T, n_fft, hop, win, stream()), "vqa_stft_magnitude")

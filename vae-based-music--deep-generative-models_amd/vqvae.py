@@ -182,8 +182,8 @@ class VQVAE:
             row_offset, n_global = vqa_dp.global_row_range(n_loc, self.process_group)
             q, _ = vq.forward(z, training=True, row_offset=row_offset, n_global=n_global, save=training_grads)
             r = dec.forward(q, save=training_grads)
-            spec, dr_spec = multispectral_loss_and_grad(target, r)
-            self.loss_slots[l, 2].copy_(spec)
+            _, dr_spec = multispectral_loss_and_grad(target, r, loss_out=self.loss_slots[l, 2:3],
+                                                     need_grad=training_grads)
             dr = torch.empty_like(r)
             V.mse_loss(x, r, dr_spec, dr, self.loss_slots[l, 0:1])
             if training_grads:
@@ -297,7 +297,8 @@ class VQVAE:
             for l in range(self.levels):
                 r = self._level_forward_only(x, l, training)
                 recons.append(r)
-                spec, _ = multispectral_loss_and_grad(target, r)
+                spec, _ = multispectral_loss_and_grad(target, r, need_grad=False)
+                spec = spec[0]
                 recon = ((x - r) ** 2).mean()
                 commit = self.vqs[l].commit[0].clone()
                 out["level_losses"].append(recon + commit + spec)
