@@ -132,6 +132,12 @@ int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t st
  * Replaces get_code_indices, VectorQuantizer.py:170-186. min_dist nullable. z is (N, D) in dtype. */
 int vqa_vq_argmin(const void* z, const float* E, const float* e_sqnorm, int64_t* idx, float* min_dist,
                   int64_t N, int D, int K, int dtype, vqa_stream_t stream);
+/* The same argmin for bf16 z (D in {32, 64}) on bf16 MFMA: E3 (K, 3, D) bf16 holds hi, mid, lo planes with
+ * hi + mid + lo = E exactly (vqa_vq_split_bf16x3, run after every codebook update), so each z.e is a sum of
+ * exact products accumulated in fp32, as with the fp32 path. */
+int vqa_vq_argmin_split(const void* z, const void* E3, const float* e_sqnorm, int64_t* idx, float* min_dist,
+                        int64_t N, int D, int K, vqa_stream_t stream);
+int vqa_vq_split_bf16x3(const float* E, void* E3, int D, int K, vqa_stream_t stream);
 /* q = ET[idx] (one_hot @ E^T, :86-90); q_st = z + (q - z) (:114);
  * commit_out[0] = beta * mean((q - z)^2) (:97-99);
  * if m_sumT != NULL: m_sumT[k][d] += sum_{n: idx[n]=k} z[n][d], n_sum[k] += count (:123-124; the

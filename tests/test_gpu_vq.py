@@ -50,6 +50,54 @@ def test_argmin_exact(cuda, D, K, N, dt):
     assert torch.allclose(mind.cpu().double(), d.gather(1, got[:, None]).squeeze(1), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("D,K,N", [(64, 2048, 262144), (64, 2048, 20000), (64, 256, 2048), (32, 1024, 777),
+                                   (64, 100, 333), (32, 70, 300)])
+def test_argmin_split_exact(cuda, D, K, N):
+    """bf16 z on bf16 MFMA with the exact hi/mid/lo planes of E: same indices as the fp32 path and the fp64
+    reference on every clear row, ragged N and K (not multiples of the 256-row / 64-code tiles)."""
+    g = torch.Generator().manual_seed(D * 13 + K + N)
+    z = torch.randn(N, D, generator=g).to(torch.bfloat16)
+    E = (torch.rand(D, K, generator=g) - 0.5) * 0.1 + 0.05 * torch.randn(D, K, generator=g)
+    zd, Ed = z.to(cuda), E.to(cuda)
+    esq = torch.empty(K, device=cuda)
+    V.vq_sqnorm(Ed, esq)
+    E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=cuda)
+    V.vq_split_bf16x3(Ed, E3)
+    # the planes reconstruct E exactly
+    P = E3.float().cpu()
+    assert torch.equal((P[:, 0] + P[:, 1] + P[:, 2]).t(), E)
+    idx = torch.empty(N, dtype=torch.int64, device=cuda)
+    mind = torch.empty(N, device=cuda)
+    V.vq_argmin_split(zd, E3, esq, idx, mind)
+    idx32 = torch.empty(N, dtype=torch.int64, device=cuda)
+    V.vq_argmin(zd, Ed, esq, idx32)
+    d = _ref_dist(z.float(), E)
+    ok = _margin_mask(d)
+    got = idx.cpu()
+    assert ok.float().mean() > 0.99
+    assert torch.equal(got[ok], d.argmin(1)[ok])
+    assert (got == idx32.cpu()).float().mean() > 0.999
+    assert torch.allclose(mind.cpu().double(), d.gather(1, got[:, None]).squeeze(1), rtol=1e-5, atol=1e-5)
+
+
+def test_argmin_split_ties_lowest_index(cuda):
+    D, K = 64, 512
+    E = torch.zeros(D, K)
+    E[:, 7] = 1.0
+    E[:, 300] = 1.0
+    z = torch.ones(40, D, dtype=torch.bfloat16)
+    z[20:] = 0.0
+    Ed = E.to(cuda)
+    esq = torch.empty(K, device=cuda)
+    V.vq_sqnorm(Ed, esq)
+    E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=cuda)
+    V.vq_split_bf16x3(Ed, E3)
+    idx = torch.empty(40, dtype=torch.int64, device=cuda)
+    V.vq_argmin_split(z.to(cuda), E3, esq, idx)
+    got = idx.cpu()
+    assert (got[:20] == 7).all() and (got[20:] == 0).all()
+
+
 def test_argmin_ties_lowest_index(cuda):
     D, K = 64, 512
     E = torch.zeros(D, K)

@@ -5,7 +5,8 @@ call(x, training=True) (:75-165): nearest code (get_code_indices :170-186), q = 
 commitment loss beta * mean((sg(q) - x)^2) (:97-107), straight-through x + sg(q - x) (:114), and when
 training the EMA update with dead-code reset (:116-145) and usage / entropy metrics (:149-159).
 
-MI355X path: libvqa kernels — an MFMA argmin that never materialises the N x K distances, a row gather
+MI355X path: libvqa kernels — an MFMA argmin that never materialises the N x K distances (bf16 MFMA on
+exact hi/mid/lo planes of E when z is bf16), a row gather
 from ET = E^T (the one-hot GEMM of :86-90 is a gather), atomic EMA sums (the dense GEMM of :123-124 is
 a scatter-add), and one EMA/reset kernel. The reset candidates use an injected seeded permutation in
 place of the reference's unseeded tf.random.shuffle (:137).
@@ -44,12 +45,14 @@ class VectorQuantizer:
         self.m_t = self.embeddings.clone()
         self.N_t = torch.ones(K, dtype=torch.float32, device=self.device)
         self.e_sqnorm = torch.empty(K, dtype=torch.float32, device=self.device)
+        # hi/mid/lo bf16 planes of E for the bf16-MFMA argmin (exact products; vqa_vq_argmin_split)
+        self.E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=self.device)
         self.calls = torch.zeros(1, dtype=torch.int64, device=self.device)  # reset-permutation counter
         self.vq_metrics = torch.zeros(3, dtype=torch.float32, device=self.device)
         self.commit = torch.zeros(1, dtype=torch.float32, device=self.device)
         # EMA statistics: own buffers unless a model binds them into its all-reduce bucket
         self.bind_stats(torch.zeros(self.stats_size(), dtype=torch.float32, device=self.device))
-        V.vq_sqnorm(self.embeddings, self.e_sqnorm)
+        self._codebook_changed()
         # TF multiplies float32 tensors by the python floats gamma and (1. - gamma) (:128,:131)
         self._g = float(np.float32(decay_rate))
         self._omg = float(np.float32(1.0 - decay_rate))
@@ -75,12 +78,23 @@ class VectorQuantizer:
         self.n_sum = buf[K * D:K * D + K]
         self.RT = buf[K * D + K:].view(K, D)
 
+    def _codebook_changed(self):
+        """Derived codebook state after every change of E: |e_k|^2 and the bf16 planes."""
+        V.vq_sqnorm(self.embeddings, self.e_sqnorm)
+        V.vq_split_bf16x3(self.embeddings, self.E3)
+
+    def _argmin(self, flat: torch.Tensor, idx: torch.Tensor, min_dist=None):
+        if flat.dtype == torch.bfloat16 and self.embedding_dim in (32, 64):
+            V.vq_argmin_split(flat, self.E3, self.e_sqnorm, idx, min_dist)
+        else:
+            V.vq_argmin(flat, self.embeddings, self.e_sqnorm, idx, min_dist)
+
     # ---- reference API ----
     def get_code_indices(self, flattened_inputs: torch.Tensor) -> torch.Tensor:
         """VectorQuantizer.py:170-186 -> (N,) int64, ties to the lowest index."""
         flat = flattened_inputs.contiguous()
         idx = torch.empty(flat.shape[0], dtype=torch.int64, device=flat.device)
-        V.vq_argmin(flat, self.embeddings, self.e_sqnorm, idx)
+        self._argmin(flat, idx)
         return idx
 
     def get_usage_count(self):
@@ -112,7 +126,7 @@ class VectorQuantizer:
         flat = z.reshape(-1, D)
         N = flat.shape[0]
         idx = torch.empty(N, dtype=torch.int64, device=z.device)
-        V.vq_argmin(flat, self.embeddings, self.e_sqnorm, idx)
+        self._argmin(flat, idx)
         q = torch.empty_like(flat)
         V.vq_quantize(flat, self.ET, idx, q, self.commit, self.m_sumT if training else None,
                       self.n_sum if training else None, self.beta)
@@ -134,7 +148,7 @@ class VectorQuantizer:
     def apply_ema(self, update_trackers: bool = True):
         V.vq_ema_apply(self.embeddings, self.ET, self.m_t, self.N_t, self.m_sumT, self.n_sum, self.RT, self._g,
                        self._omg, float(self.codebook_usage_threshold), self.vq_metrics, self.calls)
-        V.vq_sqnorm(self.embeddings, self.e_sqnorm)
+        self._codebook_changed()
         if update_trackers:
             self.batch_usage_tracker.update_state(self.vq_metrics[0])
             self.usage_tracker.update_state(self.vq_metrics[1])
@@ -151,4 +165,4 @@ class VectorQuantizer:
         self.m_t.copy_(torch.as_tensor(np.asarray(st["m_t"], np.float32)))
         self.N_t.copy_(torch.as_tensor(np.asarray(st["N_t"], np.float32)))
         self.calls.fill_(int(st.get("calls", 0)))
-        V.vq_sqnorm(self.embeddings, self.e_sqnorm)
+        self._codebook_changed()

@@ -116,6 +116,143 @@ __global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const f
     }
 }
 
+// ---- argmin for bf16 z on bf16 MFMA, exact to fp32 products ----------------------------------------
+// E is split once per codebook update into three bf16 planes hi + mid + lo (= E exactly: 3 x 8 mantissa
+// bits) and z (bf16) is exact in bf16, so z.e = z.lo + z.mid + z.hi sums exact products with fp32
+// accumulation — the same quality as the fp32 FMA chain at 3/16 of the MFMA time (16x16x32 bf16 vs
+// 16x16x4 f32). The distance and the tie rule are those of vq_argmin_mfma_kernel.
+// WG = 4 waves x 64 rows; code chunks of KC codes (3 planes, padded rows) staged in LDS.
+constexpr int kSplitKC = 64;
+
+template <int D>
+__global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, const bf16* E3, const float* esq,
+                                                             int64_t* idx, float* mind, long long N, int K) {
+  constexpr int KC = kSplitKC, KS = D / 32, RT = 4;
+  constexpr int CS = 3 * D + 8;          // LDS code stride (bf16): +16 B so 16 codes hit distinct banks
+  constexpr int PPC = 3 * D * 2 / 16;    // 16-byte pieces per code
+  __shared__ __attribute__((aligned(16))) bf16 El[KC * CS];
+  __shared__ float el2[KC];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long n0 = (long long)blockIdx.x * 256 + wave * 64;
+
+  bf16x8 af[RT][KS];
+  float zq[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const long long row = n0 + rt * 16 + (lane & 15);
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 v;
+      if (row < N) {
+        v = *(const bf16x8*)(z + row * D + ks * 32 + 8 * (lane >> 4));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)0.f;
+      }
+      af[rt][ks] = v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (float)v[j];
+        s += f * f;
+      }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(s, 4 * (lane >> 4) + r, 64);
+  }
+
+  float best[RT][4];
+  int bidx[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      best[rt][r] = __builtin_inff();
+      bidx[rt][r] = 0x7fffffff;
+    }
+
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < KC * PPC; e += 256) {
+      const int c = e / PPC, p = e - c * PPC;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (k0 + c < K) v = *(const uint4*)(E3 + (size_t)(k0 + c) * 3 * D + p * 8);
+      *(uint4*)(El + c * CS + p * 8) = v;
+    }
+    for (int e = threadIdx.x; e < KC; e += 256) el2[e] = (k0 + e < K) ? esq[k0 + e] : 0.f;
+    __syncthreads();
+#pragma unroll 1
+    for (int ct = 0; ct < KC / 16; ++ct) {
+      const int kl = ct * 16 + (lane & 15);
+      const bf16* eb = El + kl * CS + 8 * (lane >> 4);
+      bf16x8 bfr[3][KS];
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bfr[s][ks] = *(const bf16x8*)(eb + s * D + ks * 32);
+      const int kg = k0 + kl;
+      const float e2 = el2[kl];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 2; s >= 0; --s)  // smallest plane first
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt][ks], bfr[s][ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = zq[rt][r] + e2;
+          const float dist = t - 2.0f * acc[r];
+          if (kg < K && dist < best[rt][r]) {
+            best[rt][r] = dist;
+            bidx[rt][r] = kg;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float b = best[rt][r];
+      int bi = bidx[rt][r];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        const float ob = __shfl_xor(b, m, 64);
+        const int oi = __shfl_xor(bi, m, 64);
+        if (ob < b || (ob == b && oi < bi)) {
+          b = ob;
+          bi = oi;
+        }
+      }
+      const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
+      if ((lane & 15) == 0 && row < N) {
+        idx[row] = bi;
+        if (mind) mind[row] = b;
+      }
+    }
+}
+
+// E (D, K) fp32 -> E3 (K, 3, D) bf16 planes with hi + mid + lo = E
+__global__ __launch_bounds__(256) void vq_split3_kernel(const float* E, bf16* E3, int D, int K) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)D * K) return;
+  const int d = (int)(e / K), k = (int)(e - (long long)d * K);
+  const float v = E[e];
+  const bf16 hi = (bf16)v;
+  const float r1 = v - (float)hi;
+  const bf16 mid = (bf16)r1;
+  const bf16 lo = (bf16)(r1 - (float)mid);
+  bf16* o = E3 + (size_t)k * 3 * D + d;
+  o[0] = hi;
+  o[D] = mid;
+  o[2 * D] = lo;
+}
+
 // generic argmin (any D): one thread per row
 template <class T>
 __global__ __launch_bounds__(256) void vq_argmin_direct_kernel(const T* z, const float* E, const float* esq,
@@ -311,6 +448,32 @@ extern "C" int vqa_vq_argmin(const void* z, const float* E, const float* e_sqnor
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "vq_argmin: unknown dtype %d", dtype);
   if (dtype == VQA_BF16) return launch_argmin<bf16>(z, E, e_sqnorm, idx, min_dist, N, D, K, (hipStream_t)stream);
   return launch_argmin<float>(z, E, e_sqnorm, idx, min_dist, N, D, K, (hipStream_t)stream);
+}
+
+extern "C" int vqa_vq_split_bf16x3(const float* E, void* E3, int D, int K, vqa_stream_t stream) {
+  VQA_ARG(E && E3 && D > 0 && K > 0, "vq_split_bf16x3: bad arguments");
+  const long long n = (long long)D * K;
+  hipLaunchKernelGGL(vq_split3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, E,
+                     (bf16*)E3, D, K);
+  VQA_LAUNCHED("vq_split3_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_vq_argmin_split(const void* z, const void* E3, const float* e_sqnorm, int64_t* idx, float* min_dist,
+                                   int64_t N, int D, int K, vqa_stream_t stream) {
+  VQA_ARG(z && E3 && e_sqnorm && idx, "vq_argmin_split: null pointer");
+  VQA_ARG(N > 0 && K > 0 && (D == 32 || D == 64), "vq_argmin_split: bad shape N=%lld D=%d K=%d (D in {32, 64})",
+          (long long)N, D, K);
+  const dim3 g((unsigned)((N + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64)
+    hipLaunchKernelGGL(vq_argmin_split_kernel<64>, g, dim3(256), 0, s, (const bf16*)z, (const bf16*)E3, e_sqnorm, idx,
+                       min_dist, (long long)N, K);
+  else
+    hipLaunchKernelGGL(vq_argmin_split_kernel<32>, g, dim3(256), 0, s, (const bf16*)z, (const bf16*)E3, e_sqnorm, idx,
+                       min_dist, (long long)N, K);
+  VQA_LAUNCHED("vq_argmin_split_kernel");
+  return VQA_OK;
 }
 
 extern "C" size_t vqa_vq_quantize_workspace(int64_t N, int D, int K, int dtype) {

@@ -29,6 +29,7 @@ EXPORTED = [
     "vqa_conv1d_bwd_weight_partials", "vqa_conv1d_transpose_bwd_weight_partials", "vqa_reduce_partials",
     "vqa_conv1d_bwd_data_weight", "vqa_conv1d_bwd_data_weight_workspace",
     "vqa_spectral_loss", "vqa_spectral_loss_workspace", "vqa_stft_magnitude",
+    "vqa_vq_argmin_split", "vqa_vq_split_bf16x3",
 ]
 
 
@@ -80,6 +81,8 @@ _SIGS = {
     "vqa_spectral_loss": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _S, _P]),
     "vqa_spectral_loss_workspace": (_S, [_I, _I, _P, _P, _P, _I, _I]),
     "vqa_stft_magnitude": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "vqa_vq_argmin_split": (_I, [_P, _P, _P, _P, _P, _L, _I, _I, _P]),
+    "vqa_vq_split_bf16x3": (_I, [_P, _P, _I, _I, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -253,6 +256,22 @@ def vq_argmin(z, E, esq, idx, min_dist=None):
     K = E.shape[1]
     _check(lib().vqa_vq_argmin(ptr(z), ptr(E), ptr(esq), ptr(idx), ptr(min_dist), N, D, K, dtype_code(z.dtype),
                                stream()), "vqa_vq_argmin")
+
+
+def vq_split_bf16x3(E, E3):
+    D, K = E.shape
+    if tuple(E3.shape) != (K, 3, D) or E3.dtype != torch.bfloat16:
+        raise VQAError(f"vq_split_bf16x3: E3 must be ({K}, 3, {D}) bf16")
+    _check(lib().vqa_vq_split_bf16x3(ptr(E), ptr(E3), D, K, stream()), "vqa_vq_split_bf16x3")
+
+
+def vq_argmin_split(z, E3, esq, idx, min_dist=None):
+    N, D = z.shape
+    K = E3.shape[0]
+    if z.dtype != torch.bfloat16:
+        raise VQAError("vq_argmin_split takes bf16 z")
+    _check(lib().vqa_vq_argmin_split(ptr(z), ptr(E3), ptr(esq), ptr(idx), ptr(min_dist), N, D, K, stream()),
+           "vqa_vq_argmin_split")
 
 
 def vq_quantize(z, ET, idx, q_st, commit_out, m_sumT, n_sum, beta):
