@@ -40,7 +40,11 @@ CONV_CASES = [
     (32, 32, 3, 1, 27, 1, 40),     # dilation halo wider than the signal
     (32, 64, 3, 1, 1, 2, 515),     # encoder projection
     (64, 32, 3, 1, 1, 2, 512),     # decoder pre-conv
-    (64, 1, 3, 1, 1, 2, 1024),     # decoder output conv (generic path, fp32 out)
+    (64, 1, 3, 1, 1, 2, 1024),     # decoder output conv (row-dot kernels, fp32 out)
+    (64, 1, 3, 1, 1, 3, 65536),    # ... at the cfg2 chunk length
+    (32, 1, 3, 1, 1, 2, 700),      # ragged tile, 32 channels
+    (64, 1, 3, 1, 3, 1, 300),      # dilated taps
+    (64, 1, 2, 1, 1, 2, 513),      # even kernel: SAME pads (0, 1)
     (8, 32, 3, 1, 3, 2, 256),      # generic small widths
     (32, 8, 3, 1, 1, 2, 256),
 ]

@@ -15,6 +15,14 @@ namespace vqa {
 // thread-local error text behind vqa_get_last_error()
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 
+// one-output-channel conv (vqa_conv_ends.hip): forward and fused data + weight gradient
+bool co1_supported(int C, int O, int K, int S, int D, int dtype, int flags);
+size_t co1_bwd_workspace(int C, int K);
+int co1_fwd(const void* x, const float* w, const float* bias, const void* resid, void* y, int B, int T, int C, int K,
+            int D, int P, int flags, int dtype, hipStream_t s);
+int co1_bwd(const void* dy, const float* w, const void* x, const void* resid, void* dx, int B, int T, int C, int K,
+            int D, int P, int flags, int dtype, void* ws, int* nparts, hipStream_t s);
+
 template <class T> __device__ __forceinline__ float ld(const T* p);
 template <> __device__ __forceinline__ float ld<float>(const float* p) { return *p; }
 template <> __device__ __forceinline__ float ld<bf16>(const bf16* p) { return (float)(*p); }

@@ -1710,6 +1710,12 @@ extern "C" int vqa_conv1d_fwd(const void* x, const float* w, const float* bias, 
                               int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation, int pad_left,
                               int flags, int dtype, vqa_stream_t stream) {
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_fwd: T_out %d != ceil(T_in/stride)", T_out);
+  if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags) && (dtype == VQA_F32 || dtype == VQA_BF16)) {
+    VQA_ARG(x && w && y && B > 0 && T_in > 0, "conv1d_fwd: bad arguments");
+    VQA_ARG(!(flags & VQA_ADD_RESIDUAL) || residual, "VQA_ADD_RESIDUAL without residual");
+    return co1_fwd(x, w, bias, residual, y, B, T_in, C_in, K, dilation, pad_left,
+                   flags & (VQA_PRE_RELU | VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32), dtype, (hipStream_t)stream);
+  }
   GatherArgs a{x, w, bias, residual, nullptr, y, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
                W_DIRECT, K, 0, T_out, flags & (VQA_PRE_RELU | VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32)};
   return run_gather(a, dtype, (hipStream_t)stream);
@@ -1727,6 +1733,15 @@ extern "C" int vqa_conv1d_bwd_data(const void* dy, const float* w, const void* m
                                    int B, int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation,
                                    int pad_left, int flags, int dtype, vqa_stream_t stream) {
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_data: T_out %d != ceil(T_in/stride)", T_out);
+  if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags) && (dtype == VQA_F32 || dtype == VQA_BF16)) {
+    VQA_ARG(dy && w && dx && B > 0 && T_in > 0, "conv1d_bwd_data: bad arguments");
+    VQA_ARG(!(flags & VQA_POST_MASK) || mask, "VQA_POST_MASK without mask");
+    VQA_ARG(!(flags & VQA_ADD_RESIDUAL) || residual, "VQA_ADD_RESIDUAL without residual");
+    // same kernel (and dx arithmetic) as the fused data + weight gradient, without the weight partials
+    const int f = ((flags & VQA_POST_MASK) ? VQA_PRE_RELU : 0) | (flags & (VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32));
+    return co1_bwd(dy, w, (flags & VQA_POST_MASK) ? mask : nullptr, residual, dx, B, T_in, C_in, K, dilation,
+                   pad_left, f, dtype, nullptr, nullptr, (hipStream_t)stream);
+  }
   const int f = swap_xy_flags(flags);
   if (stride == 1) {
     GatherArgs a{dy, w, nullptr, residual, mask, dx, B, T_out, T_in, C_out, C_in, K, 1, dilation,
@@ -1844,6 +1859,7 @@ extern "C" size_t vqa_conv1d_bwd_data_weight_workspace(int B, int T_in, int T_ou
                                                        int stride, int dilation, int pad_left, int flags, int dtype) {
   size_t need = wgrad_ws(dtype, B, T_in, T_out, C_in, C_out, K, stride, dilation,
                          flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32));
+  if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags)) need = std::max(need, co1_bwd_workspace(C_in, K));
   if (stride == 1) {
     const GatherArgs a = fused_bwd_args(nullptr, nullptr, nullptr, nullptr, nullptr, B, T_in, T_out, C_in, C_out, K,
                                         dilation, pad_left, flags);
@@ -1861,6 +1877,25 @@ extern "C" int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const 
   VQA_ARG(dy && w && x && dx && dw, "conv1d_bwd_data_weight: null tensor pointer");
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
   const hipStream_t s = (hipStream_t)stream;
+  if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags)) {
+    const size_t need = co1_bwd_workspace(C_in, K);
+    VQA_ARG(workspace && ws_bytes >= need, "workspace too small: need %zu bytes, got %zu", need, ws_bytes);
+    VQA_ARG(!(flags & VQA_ADD_RESIDUAL) || residual, "VQA_ADD_RESIDUAL without residual");
+    int nparts = 0;
+    const int rc = co1_bwd(dy, w, x, residual, dx, B, T_in, C_in, K, dilation, pad_left,
+                           flags & (VQA_PRE_RELU | VQA_ADD_RESIDUAL | VQA_X_F32 | VQA_Y_F32), dtype, workspace,
+                           &nparts, s);
+    if (rc != VQA_OK) return rc;
+    const int KCO = K * C_in, E = KCO + 1;
+    if (desc) {
+      *desc = vqa_partials_desc{(const float*)workspace, dw, db, nparts, E, KCO, 0};
+      return VQA_OK;
+    }
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((E + 63) / 64), dim3(256), 0, s, (const float*)workspace, nparts, E,
+                       KCO, dw, db);
+    VQA_LAUNCHED("reduce_partials_kernel");
+    return VQA_OK;
+  }
   if (stride == 1) {
     GatherArgs a = fused_bwd_args(dy, w, x, residual, dx, B, T_in, T_out, C_in, C_out, K, dilation, pad_left, flags);
     if (const int pvx = conv32_pvx(a, dtype, true)) {

@@ -170,8 +170,7 @@ class Decoder(Layer):
     def backward(self, dy):
         x = self._saved
         self._saved = None
-        self.out.backward_weight(x, dy, self.cdt)
-        g = self.out.backward_data(dy, x.shape[1], self.cdt)
+        g = self.out.backward_data_weight(dy, x, self.cdt)  # one pass: dx and dW/db (vqa_conv_ends.hip)
         for blk in reversed(self.blocks):
             g = blk.backward(g)
         return g
