@@ -125,6 +125,20 @@ int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const void* x, co
 size_t vqa_conv1d_bwd_data_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K, int stride,
                                             int dilation, int pad_left, int flags, int dtype);
 
+/* ---- fused residual block: replaces resnet.py:7-29 ResnetConv1DBlock (C = 32):
+ *      h = conv_a(relu(x)) + b_a (k3, dilation), y = x + conv_b(relu(h)) + b_b (k3, dilation 1), SAME padding.
+ * Weights in Keras layout (3, C, C). The forward keeps h on chip; h_out (nullable) receives relu(h).
+ * The backward recomputes h from x, so it reads dy and x and writes dx = d loss / d x; the four weight
+ * gradients (overwritten) are reduced from per-workgroup partials — or, with desc != NULL (2 entries:
+ * conv_a, conv_b), left for a later vqa_reduce_partials call. */
+int vqa_resblock_supported(int C, int dilation, int dtype);
+int vqa_resblock_fwd(const void* x, const float* wa, const float* ba, const float* wb, const float* bb, void* y,
+                     void* h_out, int B, int T, int C, int dilation, int dtype, vqa_stream_t stream);
+int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, const float* ba, const float* wb, const float* bb,
+                     void* dx, float* dwa, float* dba, float* dwb, float* dbb, int B, int T, int C, int dilation,
+                     int dtype, void* workspace, size_t ws_bytes, vqa_partials_desc* desc, vqa_stream_t stream);
+size_t vqa_resblock_bwd_workspace(int B, int T, int C, int dilation, int dtype);
+
 /* ---- Vector quantizer (VectorQuantizer.py) ---------------------------------------------------- */
 /* e_sqnorm[k] = sum_d E[d][k]^2  (VectorQuantizer.py:180). E is (D, K). */
 int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream);

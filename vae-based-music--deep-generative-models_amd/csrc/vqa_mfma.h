@@ -1,0 +1,91 @@
+// vqa_mfma.h — MFMA fragment traits and bit-level ReLU helpers shared by the conv kernels (gfx950).
+#pragma once
+#include "vqa_common.h"
+
+namespace vqa {
+
+// MFMA fragment traits. bf16: v_mfma_f32_16x16x32_bf16 (8 consecutive channels per lane, one
+// 16-byte LDS read). fp32: v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain; used for parity runs).
+template <class T> struct Mfma;
+template <> struct Mfma<bf16> {
+  static constexpr int KS = 32;
+  typedef bf16x8 frag;
+  static __device__ __forceinline__ int koff(int lane) { return 8 * (lane >> 4); }
+  static __device__ __forceinline__ frag load(const bf16* p) { return *(const bf16x8*)p; }
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  // 8 elements with a row stride (strided LDS gather; used by the weight-gradient kernel)
+  static __device__ __forceinline__ frag gather(const bf16* p, int stride) {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = p[j * stride];
+    return f;
+  }
+  static __device__ __forceinline__ frag ones() {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (bf16)1.0f;
+    return f;
+  }
+  // operand whose K index runs down the rows of a row-major LDS tile: lane l gets rows 8(l>>4) .. +7 of
+  // column l&15 from `o` = &tile[row0][col0] — two ds_read_b64_tr_b16 (cdna_hip_programming.md T10);
+  // the caller keeps EXEC full and the row stride a multiple of 8 bytes
+  static __device__ __forceinline__ frag rows(const bf16* o, int stride) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    const int l = threadIdx.x & 63, i = l & 15;
+    const bf16* a0 = o + (8 * (l >> 4) + (i >> 2)) * stride + 4 * (i & 3);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * stride));
+    frag f;
+    const bf16* pl = (const bf16*)&lo;
+    const bf16* ph = (const bf16*)&hi;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = pl[j];
+      f[j + 4] = ph[j];
+    }
+    return f;
+  }
+};
+template <> struct Mfma<float> {
+  static constexpr int KS = 4;
+  typedef float frag;
+  static __device__ __forceinline__ int koff(int lane) { return lane >> 4; }
+  static __device__ __forceinline__ frag load(const float* p) { return *p; }
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag gather(const float* p, int) { return *p; }
+  static __device__ __forceinline__ frag ones() { return 1.0f; }
+  static __device__ __forceinline__ frag rows(const float* o, int stride) {
+    const int l = threadIdx.x & 63;
+    return o[(l >> 4) * stride + (l & 15)];
+  }
+};
+
+template <class T> __device__ __forceinline__ void relu_bits(uint4& v);
+template <> __device__ __forceinline__ void relu_bits<bf16>(uint4& v) {
+  uint32_t* w = (uint32_t*)&v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] &= ~(((w[i] >> 15) & 0x00010001u) * 0xFFFFu);
+}
+template <> __device__ __forceinline__ void relu_bits<float>(uint4& v) {
+  uint32_t* w = (uint32_t*)&v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] &= ~(uint32_t)((int32_t)w[i] >> 31);
+}
+
+template <class T> constexpr int lds_pad() { return 16 / (int)sizeof(T); }
+
+__device__ __forceinline__ bf16x8 relu_frag(bf16x8 f) {
+  uint4 u = *(uint4*)&f;
+  relu_bits<bf16>(u);
+  return *(bf16x8*)&u;
+}
+__device__ __forceinline__ float relu_frag(float f) {
+  const int32_t b = __float_as_int(f);
+  return __int_as_float(b & ~(b >> 31));
+}
+
+}  // namespace vqa

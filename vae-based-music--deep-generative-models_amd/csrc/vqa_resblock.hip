@@ -1,0 +1,442 @@
+// vqa_resblock.hip — the fused residual block of the dilated ResNet stacks (gfx950).
+//
+// Replaces resnet.py:7-29 ResnetConv1DBlock for C = 32 channels:
+//     h = conv_a(relu(x)) + b_a       (k3, dilation d, SAME)
+//     y = x + conv_b(relu(h)) + b_b   (k3, dilation 1, SAME)
+// and its GradientTape backward (vqvae.py:143).
+//
+// Forward: one workgroup tile = 128 output rows; x (with a d+1 row halo) is staged once in LDS, h is
+// computed for the 144 rows conv_b needs and kept in LDS (relu'd, in the activation dtype — the same
+// rounding as the unfused path's h tensor), then y = x + conv_b(relu h) is written. HBM traffic: x read,
+// y written — h never leaves the chip.
+// Backward (recompute): h is recomputed from x instead of being saved, so the block's backward reads dy
+// and x and writes dx only:
+//     dh = conv_b^T(dy) * (h > 0)            over rows [t0-d, t0+128+d) (conv_a^T's halo)
+//     dx = dy + conv_a^T(dh) * (x > 0)       over the tile's 128 rows
+//     dW_b += relu(h)^T dy,  dW_a += relu(x)^T dh (shifted per tap), db_b += sum dy, db_a += sum dh
+// the weight gradients accumulate in registers across the persistent workgroup's tiles and leave as one
+// fp32 partial row per workgroup (reduced in a fixed order by vqa_reduce_partials: deterministic).
+// All products are MFMA (bf16 16x16x32 or the exact fp32 16x16x4 in parity mode), fp32 accumulation.
+#include "vqa_common.h"
+#include "vqa_mfma.h"
+
+namespace vqa {
+
+constexpr int RC = 32;    // block width (residual_width of the SMALL_VQ_VAE configs)
+constexpr int RTM = 128;  // output rows per tile
+constexpr int RMAXD = 32; // largest dilation the LDS plan covers (the model uses 1, 3, 9, 27)
+
+struct ResArgs {
+  const void* x;   // block input (B, T, C)
+  const void* dy;  // backward: d loss / d y
+  void* y;         // forward: y; backward: dx
+  void* h;         // forward, optional: relu(h) of the tile's own rows (B, T, C)
+  const float* wa;
+  const float* ba;
+  const float* wb;
+  const float* bb;
+  float* part_a;  // backward: [nwg][3*C*C + C] (dW_a | db_a)
+  float* part_b;  // backward: [nwg][3*C*C + C] (dW_b | db_b)
+  int B, T, d;
+  int ntm, ntiles, tpw;
+};
+
+template <class T> constexpr int rs_stride() { return RC + lds_pad<T>(); }
+constexpr int round16(int v) { return (v + 15) & ~15; }
+
+// weights -> LDS image [3][32][WS]: TRANSPOSE=true gives [k][o][c] (A operand of a forward conv),
+// false the Keras layout [k][c][o] (A operand of the transposed conv)
+template <class T, bool TRANSPOSE>
+__device__ __forceinline__ void stage_wimg(T* img, const float* w) {
+  constexpr int WS = rs_stride<T>();
+  for (int e = threadIdx.x; e < 3 * RC * RC; e += 256) {
+    const int k = e / (RC * RC), rem = e - k * RC * RC, r = rem / RC, c = rem - r * RC;
+    // e enumerates the Keras layout: w[k][r][c] with r = input channel, c = output channel
+    if (TRANSPOSE) img[(k * RC + c) * WS + r] = (T)w[e];
+    else img[(k * RC + r) * WS + c] = (T)w[e];
+  }
+}
+
+// rows [row0, row0 + nrows) of one item (32 channels) -> LDS rows of stride XS; rows outside [0, Tlen) = 0.
+// Loads of a batch are issued before its stores (branch-free addresses).
+template <class T>
+__device__ __forceinline__ void stage_rows32(T* dst, const T* src, int row0, int nrows, int Tlen) {
+  constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC, XS = rs_stride<T>();
+  const int n = nrows * CPR;
+  for (int base = 0; base < n; base += 4 * 256) {
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = base + threadIdx.x + i * 256;
+      const int rr = e / CPR, q = e - rr * CPR, r = row0 + rr;
+      const bool ok = e < n && r >= 0 && r < Tlen;
+      v[i] = *((const uint4*)(src + (size_t)(ok ? r : 0) * RC) + (ok ? q : 0));
+      if (!ok) v[i] = uint4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = base + threadIdx.x + i * 256;
+      if (e < n) {
+        const int rr = e / CPR, q = e - rr * CPR;
+        *(uint4*)(dst + rr * XS + q * VEC) = v[i];
+      }
+    }
+  }
+}
+
+// acc[mt] (16 output channels each) for 16 output rows: out[row][o] = sum_k sum_c img[k][o][c] *
+// act(in[row_base + k*tap_step + row][c]); lane: row = lane & 15, channels mt*16 + 4*(lane>>4) + 0..3.
+// Tap order k = 0, 1, 2 then channel blocks — the accumulation order of the unfused gather kernels.
+template <class T, bool RELU_IN>
+__device__ __forceinline__ void conv_rows16(f32x4 (&acc)[2], const T* img, const T* in, int row_base, int tap_step) {
+  typedef Mfma<T> M;
+  constexpr int WS = rs_stride<T>(), XS = rs_stride<T>();
+  const int lane = threadIdx.x & 63, ko = M::koff(lane);
+  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const T* wk = img + (k * RC + (lane & 15)) * WS + ko;
+    const T* xr = in + (row_base + k * tap_step + (lane & 15)) * XS + ko;
+#pragma unroll
+    for (int cc = 0; cc < RC; cc += M::KS) {
+      const typename M::frag a0 = M::load(wk + cc), a1 = M::load(wk + 16 * WS + cc);
+      typename M::frag b = M::load(xr + cc);
+      if (RELU_IN) b = relu_frag(b);
+      acc[0] = M::mma(a0, b, acc[0]);
+      acc[1] = M::mma(a1, b, acc[1]);
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o], b[o + 1], b[o + 2], b[o + 3]}; }
+
+// ---------------------------------------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
+  constexpr int WS = rs_stride<T>(), XS = WS, HR = RTM + 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* wa_img = (T*)smem;
+  T* wb_img = wa_img + 3 * RC * WS;
+  T* X = wb_img + 3 * RC * WS;  // local j <-> row t0 - 1 - d + j, XR = HR + 2d rows (raw x)
+  const int d = a.d, XR = HR + 2 * d;
+  T* H = X + XR * XS;  // local i <-> row t0 - 1 + i, relu(h)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
+  if (tbeg >= tend) return;
+  stage_wimg<T, true>(wa_img, a.wa);
+  stage_wimg<T, true>(wb_img, a.wb);
+  f32x4 bav[2], bbv[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int o = mt * 16 + 4 * (lane >> 4);
+    bav[mt] = a.ba ? bias4(a.ba, o) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bbv[mt] = a.bb ? bias4(a.bb, o) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int tile = tbeg; tile < tend; ++tile) {
+    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
+    const T* xi = (const T*)a.x + (size_t)n * a.T * RC;
+    __syncthreads();
+    stage_rows32<T>(X, xi, t0 - 1 - d, XR, a.T);
+    __syncthreads();
+    // h rows t0-1 .. t0+142 (conv_b reads t0-1 .. t0+128); rows outside the item are conv_b's SAME zeros
+    for (int nt = wave; nt < HR / 16; nt += 4) {
+      f32x4 acc[2];
+      conv_rows16<T, true>(acc, wa_img, X, nt * 16, d);
+      const int i = nt * 16 + (lane & 15), r = t0 - 1 + i;
+      const bool live = r >= 0 && r < a.T;
+      const bool own = a.h && live && i >= 1 && i <= RTM;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x4 v = acc[mt] + bav[mt];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
+        st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
+        if (own) st4((T*)a.h + ((size_t)n * a.T + r) * RC + mt * 16 + 4 * (lane >> 4), v);
+      }
+    }
+    __syncthreads();
+    T* yi = (T*)a.y + (size_t)n * a.T * RC;
+    for (int nt = wave; nt < RTM / 16; nt += 4) {
+      f32x4 acc[2];
+      conv_rows16<T, false>(acc, wb_img, H, nt * 16, 1);
+      const int tl = nt * 16 + (lane & 15), t = t0 + tl;
+      if (t < a.T) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int o = mt * 16 + 4 * (lane >> 4);
+          f32x4 v = acc[mt] + bbv[mt];
+          v = ld4(X + (tl + 1 + d) * XS + o) + v;
+          st4(yi + (size_t)t * RC + o, v);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
+  typedef Mfma<T> M;
+  constexpr int WS = rs_stride<T>(), XS = WS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int d = a.d, HR = round16(RTM + 2 * d), XR = HR + 2 * d, YR = HR + 2;
+  T* waF = (T*)smem;            // conv_a forward (recompute h): [k][o][c]
+  T* waT = waF + 3 * RC * WS;   // conv_a^T: Keras [k][c][o]
+  T* wbT = waT + 3 * RC * WS;   // conv_b^T: Keras [k][c][o]
+  T* X = wbT + 3 * RC * WS;     // local j <-> row t0 - 2d + j (raw x)
+  T* Y = X + XR * XS;           // local m <-> row t0 - d - 1 + m (dy)
+  T* H = Y + YR * XS;           // local i <-> row t0 - d + i: relu(h), then dh
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
+  if (tbeg >= tend) return;
+  stage_wimg<T, true>(waF, a.wa);
+  stage_wimg<T, false>(waT, a.wa);
+  stage_wimg<T, false>(wbT, a.wb);
+  f32x4 bav[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) bav[mt] = a.ba ? bias4(a.ba, mt * 16 + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // weight-gradient accumulators: wave w owns input-channel tile ct = w >> 1, output-channel tile ot = w & 1
+  const int ct = wave >> 1, ot = wave & 1;
+  f32x4 gwa[3], gwb[3], gba = {0.f, 0.f, 0.f, 0.f}, gbb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    gwa[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gwb[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int nht = HR / 16;  // <= 12
+
+  for (int tile = tbeg; tile < tend; ++tile) {
+    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
+    __syncthreads();
+    stage_rows32<T>(X, (const T*)a.x + (size_t)n * a.T * RC, t0 - 2 * d, XR, a.T);
+    stage_rows32<T>(Y, (const T*)a.dy + (size_t)n * a.T * RC, t0 - d - 1, YR, a.T);
+    __syncthreads();
+    // 1. recompute relu(h) over the dh rows (zero outside the item)
+    for (int nt = wave; nt < nht; nt += 4) {
+      f32x4 acc[2];
+      conv_rows16<T, true>(acc, waF, X, nt * 16, d);
+      const int i = nt * 16 + (lane & 15), r = t0 - d + i;
+      const bool live = r >= 0 && r < a.T;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x4 v = acc[mt] + bav[mt];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
+        st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
+      }
+    }
+    __syncthreads();
+    // 2a. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o], db_b += sum_t dy[t] (the tile's own rows)
+#pragma unroll 1
+    for (int kk = 0; kk < RTM; kk += M::KS) {
+      const typename M::frag bf = M::rows(Y + (d + 1 + kk) * XS + ot * 16, XS);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const typename M::frag af = M::rows(H + (d + k - 1 + kk) * XS + ct * 16, XS);
+        gwb[k] = M::mma(af, bf, gwb[k]);
+      }
+      if (ct == 0) gbb = M::mma(M::ones(), bf, gbb);
+    }
+    // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
+    f32x4 dh[3][2];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int nt = wave + 4 * s;
+      if (nt < nht) {
+        conv_rows16<T, false>(dh[s], wbT, Y, nt * 16 + 2, -1);
+        const int i = nt * 16 + (lane & 15);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const f32x4 hm = ld4(H + i * XS + mt * 16 + 4 * (lane >> 4));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dh[s][mt][q] = hm[q] > 0.f ? dh[s][mt][q] : 0.f;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int nt = wave + 4 * s;
+      if (nt < nht) {
+        const int i = nt * 16 + (lane & 15);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) st4(H + i * XS + mt * 16 + 4 * (lane >> 4), dh[s][mt]);
+      }
+    }
+    __syncthreads();
+    // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows
+    T* dxi = (T*)a.y + (size_t)n * a.T * RC;
+    for (int nt = wave; nt < RTM / 16; nt += 4) {
+      f32x4 acc[2];
+      conv_rows16<T, false>(acc, waT, H, nt * 16 + 2 * d, -d);
+      const int tl = nt * 16 + (lane & 15), t = t0 + tl;
+      if (t < a.T) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int o = mt * 16 + 4 * (lane >> 4);
+          const f32x4 xm = ld4(X + (tl + 2 * d) * XS + o);
+          f32x4 v = acc[mt];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = xm[q] > 0.f ? v[q] : 0.f;
+          v = ld4(Y + (tl + d + 1) * XS + o) + v;
+          st4(dxi + (size_t)t * RC + o, v);
+        }
+      }
+    }
+    // 4. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o], db_a += sum_t dh[t]
+#pragma unroll 1
+    for (int kk = 0; kk < RTM; kk += M::KS) {
+      const typename M::frag bf = M::rows(H + (d + kk) * XS + ot * 16, XS);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const typename M::frag af = relu_frag(M::rows(X + ((k + 1) * d + kk) * XS + ct * 16, XS));
+        gwa[k] = M::mma(af, bf, gwa[k]);
+      }
+      if (ct == 0) gba = M::mma(M::ones(), bf, gba);
+    }
+  }
+  // partial rows: Keras dW[k][c][o] (c = ct*16 + 4*(lane>>4) + r, o = ot*16 + (lane&15)), then the bias
+  float* pa = a.part_a + (size_t)blockIdx.x * (3 * RC * RC + RC);
+  float* pb = a.part_b + (size_t)blockIdx.x * (3 * RC * RC + RC);
+  const int o = ot * 16 + (lane & 15);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = ct * 16 + 4 * (lane >> 4) + r;
+      pa[(k * RC + c) * RC + o] = gwa[k][r];
+      pb[(k * RC + c) * RC + o] = gwb[k][r];
+    }
+  if (ct == 0 && lane < 16) {
+    pa[3 * RC * RC + o] = gba[0];
+    pb[3 * RC * RC + o] = gbb[0];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+static int rs_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
+  }();
+  return n;
+}
+constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the partial rows)
+
+static size_t fwd_lds(int d, int esz) {
+  const int s = RC + 16 / esz, HR = RTM + 16;
+  return ((size_t)6 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)HR * s) * esz;
+}
+static size_t bwd_lds(int d, int esz) {
+  const int s = RC + 16 / esz, HR = round16(RTM + 2 * d);
+  return ((size_t)9 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
+}
+
+static int set_lds(const void* fn, size_t bytes) {
+  static size_t done[4] = {0, 0, 0, 0};
+  static const void* fns[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (bytes <= 65536) return VQA_OK;
+  int slot = 0;
+  while (slot < 3 && fns[slot] && fns[slot] != fn) ++slot;
+  if (fns[slot] == fn && done[slot] >= bytes) return VQA_OK;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("resblock: cannot reserve %zu B of LDS", bytes);
+    return VQA_E_UNSUPPORTED;
+  }
+  fns[slot] = fn;
+  done[slot] = bytes;
+  return VQA_OK;
+}
+
+static void plan(ResArgs& a, int per_cu) {
+  a.ntm = (a.T + RTM - 1) / RTM;
+  a.ntiles = a.ntm * a.B;
+  int nwg = rs_cus() * per_cu;
+  if (nwg > a.ntiles) nwg = a.ntiles;
+  a.tpw = (a.ntiles + nwg - 1) / nwg;
+}
+
+}  // namespace vqa
+
+using namespace vqa;
+
+extern "C" int vqa_resblock_supported(int C, int dilation, int dtype) {
+  if (C != RC || dilation < 1 || dilation > RMAXD || !(dtype == VQA_F32 || dtype == VQA_BF16)) return 0;
+  const int esz = dtype == VQA_BF16 ? 2 : 4;
+  return bwd_lds(dilation, esz) <= 160 * 1024 && fwd_lds(dilation, esz) <= 160 * 1024;
+}
+
+extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba, const float* wb, const float* bb,
+                                void* y, void* h_out, int B, int T, int C, int dilation, int dtype,
+                                vqa_stream_t stream) {
+  VQA_ARG(x && wa && wb && y && B > 0 && T > 0, "resblock_fwd: bad arguments");
+  VQA_REQUIRE(vqa_resblock_supported(C, dilation, dtype), VQA_E_UNSUPPORTED,
+              "resblock_fwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
+  VQA_ARG((long long)B * T * C < (1ll << 40), "resblock_fwd: tensor too large");
+  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0};
+  plan(a, 3);
+  const int esz = dtype == VQA_BF16 ? 2 : 4;
+  const size_t lds = fwd_lds(RMAXD, esz);  // one LDS reservation for every dilation
+  const hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((a.ntiles + a.tpw - 1) / a.tpw);
+  if (dtype == VQA_BF16) {
+    if (int rc = set_lds((const void*)resblock_fwd_kernel<bf16>, lds)) return rc;
+    hipLaunchKernelGGL(resblock_fwd_kernel<bf16>, grid, dim3(256), lds, s, a);
+  } else {
+    if (int rc = set_lds((const void*)resblock_fwd_kernel<float>, lds)) return rc;
+    hipLaunchKernelGGL(resblock_fwd_kernel<float>, grid, dim3(256), lds, s, a);
+  }
+  VQA_LAUNCHED("resblock_fwd_kernel");
+  return VQA_OK;
+}
+
+extern "C" size_t vqa_resblock_bwd_workspace(int B, int T, int C, int dilation, int dtype) {
+  (void)B;
+  (void)T;
+  (void)dilation;
+  (void)dtype;
+  return (size_t)2 * rs_cus() * kResPerCU * (3 * C * C + C) * sizeof(float);
+}
+
+extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, const float* ba, const float* wb,
+                                const float* bb, void* dx, float* dwa, float* dba, float* dwb, float* dbb, int B,
+                                int T, int C, int dilation, int dtype, void* workspace, size_t ws_bytes,
+                                vqa_partials_desc* desc, vqa_stream_t stream) {
+  (void)bb;
+  VQA_ARG(dy && x && wa && wb && dx && dwa && dwb && B > 0 && T > 0, "resblock_bwd: bad arguments");
+  VQA_REQUIRE(vqa_resblock_supported(C, dilation, dtype), VQA_E_UNSUPPORTED,
+              "resblock_bwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
+  const size_t need = vqa_resblock_bwd_workspace(B, T, C, dilation, dtype);
+  VQA_ARG(workspace && ws_bytes >= need, "resblock_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+  const int E = 3 * RC * RC + RC;
+  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0};
+  plan(a, kResPerCU);
+  const int nwg = (a.ntiles + a.tpw - 1) / a.tpw;
+  a.part_b = a.part_a + (size_t)nwg * E;
+  const int esz = dtype == VQA_BF16 ? 2 : 4;
+  const size_t lds = bwd_lds(dilation, esz);
+  const size_t lds_max = bwd_lds(RMAXD, esz);
+  const hipStream_t s = (hipStream_t)stream;
+  if (dtype == VQA_BF16) {
+    if (int rc = set_lds((const void*)resblock_bwd_kernel<bf16>, lds_max)) return rc;
+    hipLaunchKernelGGL(resblock_bwd_kernel<bf16>, dim3(nwg), dim3(256), lds, s, a);
+  } else {
+    if (int rc = set_lds((const void*)resblock_bwd_kernel<float>, lds_max)) return rc;
+    hipLaunchKernelGGL(resblock_bwd_kernel<float>, dim3(nwg), dim3(256), lds, s, a);
+  }
+  VQA_LAUNCHED("resblock_bwd_kernel");
+  const vqa_partials_desc da{a.part_a, dwa, dba, nwg, E, 3 * RC * RC, 0};
+  const vqa_partials_desc dbd{a.part_b, dwb, dbb, nwg, E, 3 * RC * RC, 0};
+  if (desc) {
+    desc[0] = da;
+    desc[1] = dbd;
+    return VQA_OK;
+  }
+  const vqa_partials_desc both[2] = {da, dbd};
+  return vqa_reduce_partials(both, 2, stream);
+}

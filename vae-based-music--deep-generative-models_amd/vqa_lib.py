@@ -30,6 +30,7 @@ EXPORTED = [
     "vqa_conv1d_bwd_data_weight", "vqa_conv1d_bwd_data_weight_workspace",
     "vqa_spectral_loss", "vqa_spectral_loss_workspace", "vqa_stft_magnitude",
     "vqa_vq_argmin_split", "vqa_vq_split_bf16x3",
+    "vqa_resblock_supported", "vqa_resblock_fwd", "vqa_resblock_bwd", "vqa_resblock_bwd_workspace",
 ]
 
 
@@ -83,6 +84,10 @@ _SIGS = {
     "vqa_stft_magnitude": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "vqa_vq_argmin_split": (_I, [_P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "vqa_vq_split_bf16x3": (_I, [_P, _P, _I, _I, _P]),
+    "vqa_resblock_supported": (_I, [_I, _I, _I]),
+    "vqa_resblock_fwd": (_I, [_P] * 7 + [_I] * 5 + [_P]),
+    "vqa_resblock_bwd": (_I, [_P] * 11 + [_I] * 5 + [_P, _S, _P, _P]),
+    "vqa_resblock_bwd_workspace": (_S, [_I] * 5),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -178,7 +183,8 @@ class Deferred:
         self.descs, self.keep = [], []
 
     def add(self, desc, ws):
-        self.descs.append(desc)
+        descs = desc if isinstance(desc, (list, tuple)) else [desc]
+        self.descs.extend(descs)
         self.keep.append(ws)  # the partials must outlive the reduce launch
 
     def flush(self):
@@ -213,6 +219,30 @@ def conv1d_bwd_data_weight(dy, w, x, residual, dx, dw, db, B, T_in, T_out, C_in,
                                             stream()), "vqa_conv1d_bwd_data_weight")
     if deferred is not None:
         deferred.add(d, ws)
+
+
+def resblock_supported(C, dilation, dtype) -> bool:
+    return bool(lib().vqa_resblock_supported(C, dilation, dtype))
+
+
+def resblock_fwd(x, wa, ba, wb, bb, y, dilation, h_out=None):
+    """resnet.py:7-29 forward, fused (vqa_resblock_fwd); x, y, h_out (B, T, 32) in the compute dtype."""
+    B, T, C = x.shape
+    _check(lib().vqa_resblock_fwd(ptr(x), ptr(wa), ptr(ba), ptr(wb), ptr(bb), ptr(y), ptr(h_out), B, T, C, dilation,
+                                  dtype_code(x.dtype), stream()), "vqa_resblock_fwd")
+
+
+def resblock_bwd(dy, x, wa, ba, wb, bb, dx, dwa, dba, dwb, dbb, dilation, deferred=None):
+    """Backward of the fused block (h recomputed from x): dx and the four weight gradients."""
+    B, T, C = x.shape
+    dt = dtype_code(x.dtype)
+    ws = workspace(lib().vqa_resblock_bwd_workspace(B, T, C, dilation, dt), x.device)
+    descs = (PartialsDesc * 2)() if deferred is not None else None
+    _check(lib().vqa_resblock_bwd(ptr(dy), ptr(x), ptr(wa), ptr(ba), ptr(wb), ptr(bb), ptr(dx), ptr(dwa), ptr(dba),
+                                  ptr(dwb), ptr(dbb), B, T, C, dilation, dt, ptr(ws), ws.numel(), descs, stream()),
+           "vqa_resblock_bwd")
+    if deferred is not None:
+        deferred.add([descs[0], descs[1]], ws)
 
 
 def conv1d_transpose_bwd_weight_deferred(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, pad, flags, dtype,
