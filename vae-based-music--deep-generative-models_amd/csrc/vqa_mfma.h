@@ -37,15 +37,8 @@ template <> struct Mfma<bf16> {
     const bf16* a0 = o + (8 * (l >> 4) + (i >> 2)) * stride + 4 * (i & 3);
     const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
     const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * stride));
-    frag f;
-    const bf16* pl = (const bf16*)&lo;
-    const bf16* ph = (const bf16*)&hi;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f[j] = pl[j];
-      f[j + 4] = ph[j];
-    }
-    return f;
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    return __builtin_bit_cast(frag, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 };
 template <> struct Mfma<float> {
@@ -78,10 +71,17 @@ template <> __device__ __forceinline__ void relu_bits<float>(uint4& v) {
 
 template <class T> constexpr int lds_pad() { return 16 / (int)sizeof(T); }
 
+// ReLU of 8 bf16 lanes: a bf16 is negative iff its int16 is — one packed integer max per dword
+// (written per component: a subscripted vector element in an unrolled loop miscompiled to lane 0 only)
+__device__ __forceinline__ unsigned relu_pk2_bf16(unsigned w) {
+  typedef short v2s __attribute__((ext_vector_type(2)));
+  const v2s z = {0, 0};
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(v2s, w), z));
+}
 __device__ __forceinline__ bf16x8 relu_frag(bf16x8 f) {
-  uint4 u = *(uint4*)&f;
-  relu_bits<bf16>(u);
-  return *(bf16x8*)&u;
+  const uint4 u = __builtin_bit_cast(uint4, f);
+  return __builtin_bit_cast(bf16x8, uint4{relu_pk2_bf16(u.x), relu_pk2_bf16(u.y), relu_pk2_bf16(u.z),
+                                           relu_pk2_bf16(u.w)});
 }
 __device__ __forceinline__ float relu_frag(float f) {
   const int32_t b = __float_as_int(f);

@@ -57,32 +57,40 @@ __device__ __forceinline__ void stage_wimg(T* img, const float* w) {
   }
 }
 
-// rows [row0, row0 + nrows) of one item (32 channels) -> LDS rows of stride XS; rows outside [0, Tlen) = 0.
-// Loads of a batch are issued before its stores (branch-free addresses).
-template <class T>
-__device__ __forceinline__ void stage_rows32(T* dst, const T* src, int row0, int nrows, int Tlen) {
-  constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC, XS = rs_stride<T>();
-  const int n = nrows * CPR;
-  for (int base = 0; base < n; base += 4 * 256) {
-    uint4 v[4];
+// One tile's rows held in registers between load() (issued a whole tile ahead) and store() into LDS:
+// chunk e = threadIdx.x + i*256 of an nrows x 32-channel block, 16 bytes each. Every chunk issues its
+// load (rows outside the item read a valid dummy row and are zeroed at store time), so the PV loads go
+// out back to back and nothing waits on them until the store (cdna_hip_programming.md T14).
+template <class T, int PV>
+struct Rows32Regs {
+  static constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC;
+  uint4 v[PV];
+  unsigned ok;
+  __device__ __forceinline__ void load(const T* src, int row0, int nrows, int Tlen) {
+    ok = 0u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = base + threadIdx.x + i * 256;
+    for (int i = 0; i < PV; ++i) {
+      const int e = threadIdx.x + i * 256;
       const int rr = e / CPR, q = e - rr * CPR, r = row0 + rr;
-      const bool ok = e < n && r >= 0 && r < Tlen;
-      v[i] = *((const uint4*)(src + (size_t)(ok ? r : 0) * RC) + (ok ? q : 0));
-      if (!ok) v[i] = uint4{0u, 0u, 0u, 0u};
+      const bool val = e < nrows * CPR && r >= 0 && r < Tlen;
+      v[i] = *((const uint4*)(src + (size_t)(val ? r : 0) * RC) + (val ? q : 0));
+      ok |= val ? (1u << i) : 0u;
     }
+  }
+  __device__ __forceinline__ void store(T* dst, int nrows) const {
+    constexpr int XS = RC + 16 / (int)sizeof(T);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = base + threadIdx.x + i * 256;
-      if (e < n) {
+    for (int i = 0; i < PV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < nrows * CPR) {
         const int rr = e / CPR, q = e - rr * CPR;
-        *(uint4*)(dst + rr * XS + q * VEC) = v[i];
+        *(uint4*)(dst + rr * XS + q * VEC) = (ok & (1u << i)) ? v[i] : uint4{0u, 0u, 0u, 0u};
       }
     }
   }
-}
+};
+// chunks per thread for the largest tile of a launch (rows <= 256 at RMAXD)
+template <class T> constexpr int rs_pv() { return sizeof(T) == 2 ? 4 : 8; }
 
 // acc[mt] (16 output channels each) for 16 output rows: out[row][o] = sum_k sum_c img[k][o][c] *
 // act(in[row_base + k*tap_step + row][c]); lane: row = lane & 15, channels mt*16 + 4*(lane>>4) + 0..3.
@@ -109,23 +117,68 @@ __device__ __forceinline__ void conv_rows16(f32x4 (&acc)[2], const T* img, const
   }
 }
 
+// The same with the weights held in registers: wf[k][mt][cc-step] = A fragments of a forward conv
+// (A[m = o][K = c] = W[k][c][o], Keras layout), loaded once per workgroup by load_wfrags.
+template <class T> constexpr int rs_ncc() { return RC / Mfma<T>::KS; }
+
+template <class T>
+__device__ __forceinline__ void load_wfrags(typename Mfma<T>::frag (&wf)[3][2][rs_ncc<T>()], const float* w) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int s = 0; s < rs_ncc<T>(); ++s) {
+        const int o = mt * 16 + (lane & 15);
+        if constexpr (sizeof(T) == 2) {
+          const int c0 = s * 32 + 8 * (lane >> 4);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wf[k][mt][s][j] = (bf16)w[(k * RC + c0 + j) * RC + o];
+        } else {
+          wf[k][mt][s] = w[(k * RC + s * 4 + (lane >> 4)) * RC + o];
+        }
+      }
+}
+
+template <class T, bool RELU_IN>
+__device__ __forceinline__ void conv_rows16r(f32x4 (&acc)[2], const typename Mfma<T>::frag (&wf)[3][2][rs_ncc<T>()],
+                                             const T* in, int row_base, int tap_step) {
+  typedef Mfma<T> M;
+  constexpr int XS = rs_stride<T>();
+  const int lane = threadIdx.x & 63, ko = M::koff(lane);
+  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const T* xr = in + (row_base + k * tap_step + (lane & 15)) * XS + ko;
+#pragma unroll
+    for (int s = 0; s < rs_ncc<T>(); ++s) {
+      typename M::frag b = M::load(xr + s * M::KS);
+      if (RELU_IN) b = relu_frag(b);
+      acc[0] = M::mma(wf[k][0][s], b, acc[0]);
+      acc[1] = M::mma(wf[k][1][s], b, acc[1]);
+    }
+  }
+}
+
 __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o], b[o + 1], b[o + 2], b[o + 3]}; }
 
 // ---------------------------------------------------------------------------------------------------
 template <class T>
 __global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
-  constexpr int WS = rs_stride<T>(), XS = WS, HR = RTM + 16;
+  typedef Mfma<T> M;
+  constexpr int XS = rs_stride<T>(), HR = RTM + 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* wa_img = (T*)smem;
-  T* wb_img = wa_img + 3 * RC * WS;
-  T* X = wb_img + 3 * RC * WS;  // local j <-> row t0 - 1 - d + j, XR = HR + 2d rows (raw x)
+  T* X = (T*)smem;  // local j <-> row t0 - 1 - d + j, XR = HR + 2d rows (raw x)
   const int d = a.d, XR = HR + 2 * d;
   T* H = X + XR * XS;  // local i <-> row t0 - 1 + i, relu(h)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
   if (tbeg >= tend) return;
-  stage_wimg<T, true>(wa_img, a.wa);
-  stage_wimg<T, true>(wb_img, a.wb);
+  typename M::frag wfa[3][2][rs_ncc<T>()], wfb[3][2][rs_ncc<T>()];
+  load_wfrags<T>(wfa, a.wa);
+  load_wfrags<T>(wfb, a.wb);
   f32x4 bav[2], bbv[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
@@ -133,16 +186,19 @@ __global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
     bav[mt] = a.ba ? bias4(a.ba, o) : f32x4{0.f, 0.f, 0.f, 0.f};
     bbv[mt] = a.bb ? bias4(a.bb, o) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  auto item_x = [&](int tile) { return (const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC; };
+  auto row0 = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RTM - 1 - d; };
+  Rows32Regs<T, rs_pv<T>()> nx;
+  nx.load(item_x(tbeg), row0(tbeg), XR, a.T);
+  nx.store(X, XR);
+  if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1), XR, a.T);
+  __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
     const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
-    const T* xi = (const T*)a.x + (size_t)n * a.T * RC;
-    __syncthreads();
-    stage_rows32<T>(X, xi, t0 - 1 - d, XR, a.T);
-    __syncthreads();
     // h rows t0-1 .. t0+142 (conv_b reads t0-1 .. t0+128); rows outside the item are conv_b's SAME zeros
     for (int nt = wave; nt < HR / 16; nt += 4) {
       f32x4 acc[2];
-      conv_rows16<T, true>(acc, wa_img, X, nt * 16, d);
+      conv_rows16r<T, true>(acc, wfa, X, nt * 16, d);
       const int i = nt * 16 + (lane & 15), r = t0 - 1 + i;
       const bool live = r >= 0 && r < a.T;
       const bool own = a.h && live && i >= 1 && i <= RTM;
@@ -159,7 +215,7 @@ __global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
     T* yi = (T*)a.y + (size_t)n * a.T * RC;
     for (int nt = wave; nt < RTM / 16; nt += 4) {
       f32x4 acc[2];
-      conv_rows16<T, false>(acc, wb_img, H, nt * 16, 1);
+      conv_rows16r<T, false>(acc, wfb, H, nt * 16, 1);
       const int tl = nt * 16 + (lane & 15), t = t0 + tl;
       if (t < a.T) {
 #pragma unroll
@@ -170,6 +226,12 @@ __global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
           st4(yi + (size_t)t * RC + o, v);
         }
       }
+    }
+    if (tile + 1 < tend) {
+      __syncthreads();  // every read of X and H for this tile is done
+      nx.store(X, XR);
+      if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2), XR, a.T);
+      __syncthreads();
     }
   }
 }
@@ -207,12 +269,20 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   }
   const int nht = HR / 16;  // <= 12
 
+  auto item_off = [&](int tile) { return (size_t)(tile / a.ntm) * a.T * RC; };
+  auto tstart = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RTM; };
+  Rows32Regs<T, rs_pv<T>()> nx, ny;
+  nx.load((const T*)a.x + item_off(tbeg), tstart(tbeg) - 2 * d, XR, a.T);
+  ny.load((const T*)a.dy + item_off(tbeg), tstart(tbeg) - d - 1, YR, a.T);
+  nx.store(X, XR);
+  ny.store(Y, YR);
+  if (tbeg + 1 < tend) {
+    nx.load((const T*)a.x + item_off(tbeg + 1), tstart(tbeg + 1) - 2 * d, XR, a.T);
+    ny.load((const T*)a.dy + item_off(tbeg + 1), tstart(tbeg + 1) - d - 1, YR, a.T);
+  }
+  __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
     const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
-    __syncthreads();
-    stage_rows32<T>(X, (const T*)a.x + (size_t)n * a.T * RC, t0 - 2 * d, XR, a.T);
-    stage_rows32<T>(Y, (const T*)a.dy + (size_t)n * a.T * RC, t0 - d - 1, YR, a.T);
-    __syncthreads();
     // 1. recompute relu(h) over the dh rows (zero outside the item)
     for (int nt = wave; nt < nht; nt += 4) {
       f32x4 acc[2];
@@ -296,6 +366,16 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       }
       if (ct == 0) gba = M::mma(M::ones(), bf, gba);
     }
+    if (tile + 1 < tend) {
+      __syncthreads();  // every read of X, Y and H for this tile is done
+      nx.store(X, XR);
+      ny.store(Y, YR);
+      if (tile + 2 < tend) {
+        nx.load((const T*)a.x + item_off(tile + 2), tstart(tile + 2) - 2 * d, XR, a.T);
+        ny.load((const T*)a.dy + item_off(tile + 2), tstart(tile + 2) - d - 1, YR, a.T);
+      }
+      __syncthreads();
+    }
   }
   // partial rows: Keras dW[k][c][o] (c = ct*16 + 4*(lane>>4) + r, o = ot*16 + (lane&15)), then the bias
   float* pa = a.part_a + (size_t)blockIdx.x * (3 * RC * RC + RC);
@@ -329,7 +409,7 @@ constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the p
 
 static size_t fwd_lds(int d, int esz) {
   const int s = RC + 16 / esz, HR = RTM + 16;
-  return ((size_t)6 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)HR * s) * esz;
+  return ((size_t)(HR + 2 * d) * s + (size_t)HR * s) * esz;
 }
 static size_t bwd_lds(int d, int esz) {
   const int s = RC + 16 / esz, HR = round16(RTM + 2 * d);
