@@ -1,0 +1,5 @@
+#!/bin/bash
+# Phase ablation of the fused residual-block backward (GPU dev tool): time it with each phase skipped.
+for s in 0 1 2 4 8 16 31; do
+  echo "skip=$s $(VQA_RESBLOCK_SKIP=$s timeout -k 10 120 python tools/resblock_sweep.py --T 32768 --reps 10 2>/dev/null | grep 'd= 9')"
+done

@@ -19,6 +19,7 @@
 // All products are MFMA (bf16 16x16x32 or the exact fp32 16x16x4 in parity mode), fp32 accumulation.
 #include "vqa_common.h"
 #include "vqa_mfma.h"
+#include <stdlib.h>
 
 namespace vqa {
 
@@ -39,6 +40,7 @@ struct ResArgs {
   float* part_b;  // backward: [nwg][3*C*C + C] (dW_b | db_b)
   int B, T, d;
   int ntm, ntiles, tpw;
+  int skip;  // development ablation only (VQA_RESBLOCK_SKIP): bit p skips backward phase p (outputs wrong)
 };
 
 template <class T> constexpr int rs_stride() { return RC + lds_pad<T>(); }
@@ -57,38 +59,47 @@ __device__ __forceinline__ void stage_wimg(T* img, const float* w) {
   }
 }
 
-// One tile's rows held in registers between load() (issued a whole tile ahead) and store() into LDS:
-// chunk e = threadIdx.x + i*256 of an nrows x 32-channel block, 16 bytes each. Every chunk issues its
-// load (rows outside the item read a valid dummy row and are zeroed at store time), so the PV loads go
-// out back to back and nothing waits on them until the store (cdna_hip_programming.md T14).
+// The same through a per-item buffer descriptor: the hardware range check returns zeros for rows outside
+// [0, T) (SAME padding; negative offsets wrap past num_records), so a chunk costs one add and one
+// buffer_load, and the per-thread chunk offsets are fixed for the launch.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rs_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long p = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr int kRsOOB = -0x40000000;  // chunk offset that stays out of range for any row base
+
 template <class T, int PV>
-struct Rows32Regs {
-  static constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC;
+struct Rows32Buf {
+  static constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC, ROWB = RC * (int)sizeof(T);
   uint4 v[PV];
-  unsigned ok;
-  __device__ __forceinline__ void load(const T* src, int row0, int nrows, int Tlen) {
-    ok = 0u;
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int e = threadIdx.x + i * 256;
-      const int rr = e / CPR, q = e - rr * CPR, r = row0 + rr;
-      const bool val = e < nrows * CPR && r >= 0 && r < Tlen;
-      v[i] = *((const uint4*)(src + (size_t)(val ? r : 0) * RC) + (val ? q : 0));
-      ok |= val ? (1u << i) : 0u;
-    }
-  }
-  __device__ __forceinline__ void store(T* dst, int nrows) const {
+  int goff[PV], loff[PV];  // byte offset from the tile's first row; LDS element offset (-1: none)
+  __device__ __forceinline__ void init(int nrows) {
     constexpr int XS = RC + 16 / (int)sizeof(T);
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const int e = threadIdx.x + i * 256;
-      if (e < nrows * CPR) {
-        const int rr = e / CPR, q = e - rr * CPR;
-        *(uint4*)(dst + rr * XS + q * VEC) = (ok & (1u << i)) ? v[i] : uint4{0u, 0u, 0u, 0u};
-      }
+      const int rr = e / CPR, q = e - rr * CPR;
+      const bool in = e < nrows * CPR;
+      goff[i] = in ? rr * ROWB + q * 16 : kRsOOB;
+      loff[i] = in ? rr * XS + q * VEC : -1;
     }
   }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int row0) {
+    const int base = row0 * ROWB;
+#pragma unroll
+    for (int i = 0; i < PV; ++i)
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, goff[i] + base, 0, 0));
+  }
+  __device__ __forceinline__ void store(T* dst) const {
+#pragma unroll
+    for (int i = 0; i < PV; ++i)
+      if (loff[i] >= 0) *(uint4*)(dst + loff[i]) = v[i];
+  }
 };
+
 // chunks per thread for the largest tile of a launch (rows <= 256 at RMAXD)
 template <class T> constexpr int rs_pv() { return sizeof(T) == 2 ? 4 : 8; }
 
@@ -162,11 +173,53 @@ __device__ __forceinline__ void conv_rows16r(f32x4 (&acc)[2], const typename Mfm
   }
 }
 
+// NJ 16-row n-tiles at once: every B fragment is loaded before the first MFMA, then the MFMAs run tap-major
+// over the n-tiles (2*NJ independent accumulator chains), so the LDS latency and the MFMA dependency chain
+// are hidden inside the wave. afrag(k, mt, s) supplies the A fragment (registers or an LDS image). Same
+// accumulation order per output as conv_rows16.
+template <class T, bool RELU_IN, int NJ, class AFrag>
+__device__ __forceinline__ void conv_multi(f32x4 (&acc)[NJ][2], AFrag afrag, const T* in, const int (&rb)[NJ],
+                                           int tap_step) {
+  typedef Mfma<T> M;
+  constexpr int XS = rs_stride<T>(), NCC = rs_ncc<T>();
+  const int lane = threadIdx.x & 63, ko = M::koff(lane);
+  typename M::frag b[NJ][3][NCC];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int s = 0; s < NCC; ++s) {
+        b[j][k][s] = M::load(in + (rb[j] + k * tap_step + (lane & 15)) * XS + ko + s * M::KS);
+        if (RELU_IN) b[j][k][s] = relu_frag(b[j][k][s]);
+      }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    acc[j][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int s = 0; s < NCC; ++s) {
+      const typename M::frag a0 = afrag(k, 0, s), a1 = afrag(k, 1, s);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        acc[j][0] = M::mma(a0, b[j][k][s], acc[j][0]);
+        acc[j][1] = M::mma(a1, b[j][k][s], acc[j][1]);
+      }
+    }
+}
+
 __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o], b[o + 1], b[o + 2], b[o + 3]}; }
 
 // ---------------------------------------------------------------------------------------------------
+// 3 waves/SIMD for bf16 (<= 168 VGPRs without spilling); the fp32 parity build needs more registers
+template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2; }
+
 template <class T>
-__global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_fwd_waves<T>(), 8)))
+void resblock_fwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
   constexpr int XS = rs_stride<T>(), HR = RTM + 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -186,51 +239,75 @@ __global__ __launch_bounds__(256) void resblock_fwd_kernel(ResArgs a) {
     bav[mt] = a.ba ? bias4(a.ba, o) : f32x4{0.f, 0.f, 0.f, 0.f};
     bbv[mt] = a.bb ? bias4(a.bb, o) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  auto item_x = [&](int tile) { return (const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC; };
+  const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
+  auto item_x = [&](int tile) { return rs_rsrc((const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC, ibytes); };
   auto row0 = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RTM - 1 - d; };
-  Rows32Regs<T, rs_pv<T>()> nx;
-  nx.load(item_x(tbeg), row0(tbeg), XR, a.T);
-  nx.store(X, XR);
-  if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1), XR, a.T);
+  Rows32Buf<T, rs_pv<T>()> nx;
+  nx.init(XR);
+  nx.load(item_x(tbeg), row0(tbeg));
+  nx.store(X);
+  if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1));
   __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
     const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
     // h rows t0-1 .. t0+142 (conv_b reads t0-1 .. t0+128); rows outside the item are conv_b's SAME zeros
-    for (int nt = wave; nt < HR / 16; nt += 4) {
-      f32x4 acc[2];
-      conv_rows16r<T, true>(acc, wfa, X, nt * 16, d);
-      const int i = nt * 16 + (lane & 15), r = t0 - 1 + i;
-      const bool live = r >= 0 && r < a.T;
-      const bool own = a.h && live && i >= 1 && i <= RTM;
+    const bool interior = t0 - 1 >= 0 && t0 - 1 + HR <= a.T;  // uniform: no SAME-padding rows in h
+    auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
+    auto wb_frag = [&](int k, int mt, int sc) { return wfb[k][mt][sc]; };
+    {
+      // h n-tiles wave, wave+4, wave+8 of HR/16 = 9 (an out-of-range slot computes a valid tile, unstored)
+      int rb[3];
+      f32x4 acc[3][2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        f32x4 v = acc[mt] + bav[mt];
+      for (int j = 0; j < 3; ++j) rb[j] = min(wave + 4 * j, HR / 16 - 1) * 16;
+      conv_multi<T, true, 3>(acc, wa_frag, X, rb, d);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
-        st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
-        if (own) st4((T*)a.h + ((size_t)n * a.T + r) * RC + mt * 16 + 4 * (lane >> 4), v);
+      for (int j = 0; j < 3; ++j) {
+        if (wave + 4 * j >= HR / 16) continue;
+        const int i = rb[j] + (lane & 15), r = t0 - 1 + i;
+        const bool live = interior || (r >= 0 && r < a.T);
+        const bool own = a.h && live && i >= 1 && i <= RTM;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          f32x4 v = acc[j][mt] + bav[mt];
+          if (interior) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
+          }
+          st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
+          if (own) st4((T*)a.h + ((size_t)n * a.T + r) * RC + mt * 16 + 4 * (lane >> 4), v);
+        }
       }
     }
     __syncthreads();
     T* yi = (T*)a.y + (size_t)n * a.T * RC;
-    for (int nt = wave; nt < RTM / 16; nt += 4) {
-      f32x4 acc[2];
-      conv_rows16r<T, false>(acc, wfb, H, nt * 16, 1);
-      const int tl = nt * 16 + (lane & 15), t = t0 + tl;
-      if (t < a.T) {
+    {
+      int rb[2];
+      f32x4 acc[2][2];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int o = mt * 16 + 4 * (lane >> 4);
-          f32x4 v = acc[mt] + bbv[mt];
-          v = ld4(X + (tl + 1 + d) * XS + o) + v;
-          st4(yi + (size_t)t * RC + o, v);
+      for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16;
+      conv_multi<T, false, 2>(acc, wb_frag, H, rb, 1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int tl = rb[j] + (lane & 15), t = t0 + tl;
+        if (t < a.T) {
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int o = mt * 16 + 4 * (lane >> 4);
+            f32x4 v = acc[j][mt] + bbv[mt];
+            v = ld4(X + (tl + 1 + d) * XS + o) + v;
+            st4(yi + (size_t)t * RC + o, v);
+          }
         }
       }
     }
     if (tile + 1 < tend) {
       __syncthreads();  // every read of X and H for this tile is done
-      nx.store(X, XR);
-      if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2), XR, a.T);
+      nx.store(X);
+      if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2));
       __syncthreads();
     }
   }
@@ -269,38 +346,59 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   }
   const int nht = HR / 16;  // <= 12
 
+  const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
   auto item_off = [&](int tile) { return (size_t)(tile / a.ntm) * a.T * RC; };
   auto tstart = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RTM; };
-  Rows32Regs<T, rs_pv<T>()> nx, ny;
-  nx.load((const T*)a.x + item_off(tbeg), tstart(tbeg) - 2 * d, XR, a.T);
-  ny.load((const T*)a.dy + item_off(tbeg), tstart(tbeg) - d - 1, YR, a.T);
-  nx.store(X, XR);
-  ny.store(Y, YR);
-  if (tbeg + 1 < tend) {
-    nx.load((const T*)a.x + item_off(tbeg + 1), tstart(tbeg + 1) - 2 * d, XR, a.T);
-    ny.load((const T*)a.dy + item_off(tbeg + 1), tstart(tbeg + 1) - d - 1, YR, a.T);
-  }
+  auto load_tile = [&](Rows32Buf<T, rs_pv<T>()>& bx, Rows32Buf<T, rs_pv<T>()>& by, int tile) {
+    const size_t o = item_off(tile);
+    bx.load(rs_rsrc((const T*)a.x + o, ibytes), tstart(tile) - 2 * d);
+    by.load(rs_rsrc((const T*)a.dy + o, ibytes), tstart(tile) - d - 1);
+  };
+  Rows32Buf<T, rs_pv<T>()> nx, ny;
+  nx.init(XR);
+  ny.init(YR);
+  load_tile(nx, ny, tbeg);
+  nx.store(X);
+  ny.store(Y);
+  if (tbeg + 1 < tend) load_tile(nx, ny, tbeg + 1);
   __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
     const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
     // 1. recompute relu(h) over the dh rows (zero outside the item)
-    for (int nt = wave; nt < nht; nt += 4) {
-      f32x4 acc[2];
-      conv_rows16<T, true>(acc, waF, X, nt * 16, d);
-      const int i = nt * 16 + (lane & 15), r = t0 - d + i;
-      const bool live = r >= 0 && r < a.T;
+    const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
+    const int ko = M::koff(lane);
+    auto img_frag = [&](const T* img) {
+      return [=](int k, int mt, int sc) { return M::load(img + (k * RC + mt * 16 + (lane & 15)) * WS + ko + sc * M::KS); };
+    };
+    int rh[3];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        f32x4 v = acc[mt] + bav[mt];
+    for (int j = 0; j < 3; ++j) rh[j] = min(wave + 4 * j, nht - 1) * 16;
+    if (!(a.skip & 1)) {
+      f32x4 acc[3][2];
+      conv_multi<T, true, 3>(acc, img_frag(waF), X, rh, d);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
-        st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
+      for (int j = 0; j < 3; ++j) {
+        if (wave + 4 * j >= nht) continue;
+        const int i = rh[j] + (lane & 15), r = t0 - d + i;
+        const bool live = r >= 0 && r < a.T;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          f32x4 v = acc[j][mt] + bav[mt];
+          if (interior) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
+          }
+          st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
+        }
       }
     }
     __syncthreads();
     // 2a. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o], db_b += sum_t dy[t] (the tile's own rows)
-#pragma unroll 1
-    for (int kk = 0; kk < RTM; kk += M::KS) {
+#pragma unroll 4
+    for (int kk = 0; kk < (a.skip & 2 ? 0 : RTM); kk += M::KS) {
       const typename M::frag bf = M::rows(Y + (d + 1 + kk) * XS + ot * 16, XS);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -311,53 +409,61 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     }
     // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
     f32x4 dh[3][2];
+    if (!(a.skip & 4)) {
+      int rb[3];
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int nt = wave + 4 * s;
-      if (nt < nht) {
-        conv_rows16<T, false>(dh[s], wbT, Y, nt * 16 + 2, -1);
-        const int i = nt * 16 + (lane & 15);
+      for (int j = 0; j < 3; ++j) rb[j] = rh[j] + 2;
+      conv_multi<T, false, 3>(dh, img_frag(wbT), Y, rb, -1);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int i = rh[j] + (lane & 15);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const f32x4 hm = ld4(H + i * XS + mt * 16 + 4 * (lane >> 4));
 #pragma unroll
-          for (int q = 0; q < 4; ++q) dh[s][mt][q] = hm[q] > 0.f ? dh[s][mt][q] : 0.f;
+          for (int q = 0; q < 4; ++q) dh[j][mt][q] = hm[q] > 0.f ? dh[j][mt][q] : 0.f;
         }
       }
     }
     __syncthreads();
+    if (!(a.skip & 4)) {
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int nt = wave + 4 * s;
-      if (nt < nht) {
-        const int i = nt * 16 + (lane & 15);
+      for (int j = 0; j < 3; ++j) {
+        if (wave + 4 * j >= nht) continue;
+        const int i = rh[j] + (lane & 15);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) st4(H + i * XS + mt * 16 + 4 * (lane >> 4), dh[s][mt]);
+        for (int mt = 0; mt < 2; ++mt) st4(H + i * XS + mt * 16 + 4 * (lane >> 4), dh[j][mt]);
       }
     }
     __syncthreads();
     // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows
     T* dxi = (T*)a.y + (size_t)n * a.T * RC;
-    for (int nt = wave; nt < RTM / 16; nt += 4) {
-      f32x4 acc[2];
-      conv_rows16<T, false>(acc, waT, H, nt * 16 + 2 * d, -d);
-      const int tl = nt * 16 + (lane & 15), t = t0 + tl;
-      if (t < a.T) {
+    if (!(a.skip & 8)) {
+      int rb[2];
+      f32x4 acc[2][2];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int o = mt * 16 + 4 * (lane >> 4);
-          const f32x4 xm = ld4(X + (tl + 2 * d) * XS + o);
-          f32x4 v = acc[mt];
+      for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16 + 2 * d;
+      conv_multi<T, false, 2>(acc, img_frag(waT), H, rb, -d);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = xm[q] > 0.f ? v[q] : 0.f;
-          v = ld4(Y + (tl + d + 1) * XS + o) + v;
-          st4(dxi + (size_t)t * RC + o, v);
+      for (int j = 0; j < 2; ++j) {
+        const int tl = (wave + 4 * j) * 16 + (lane & 15), t = t0 + tl;
+        if (t < a.T) {
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const int o = mt * 16 + 4 * (lane >> 4);
+            const f32x4 xm = ld4(X + (tl + 2 * d) * XS + o);
+            f32x4 v = acc[j][mt];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = xm[q] > 0.f ? v[q] : 0.f;
+            v = ld4(Y + (tl + d + 1) * XS + o) + v;
+            st4(dxi + (size_t)t * RC + o, v);
+          }
         }
       }
     }
     // 4. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o], db_a += sum_t dh[t]
-#pragma unroll 1
-    for (int kk = 0; kk < RTM; kk += M::KS) {
+#pragma unroll 4
+    for (int kk = 0; kk < (a.skip & 16 ? 0 : RTM); kk += M::KS) {
       const typename M::frag bf = M::rows(H + (d + kk) * XS + ot * 16, XS);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -368,12 +474,9 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     }
     if (tile + 1 < tend) {
       __syncthreads();  // every read of X, Y and H for this tile is done
-      nx.store(X, XR);
-      ny.store(Y, YR);
-      if (tile + 2 < tend) {
-        nx.load((const T*)a.x + item_off(tile + 2), tstart(tile + 2) - 2 * d, XR, a.T);
-        ny.load((const T*)a.dy + item_off(tile + 2), tstart(tile + 2) - d - 1, YR, a.T);
-      }
+      nx.store(X);
+      ny.store(Y);
+      if (tile + 2 < tend) load_tile(nx, ny, tile + 2);
       __syncthreads();
     }
   }
@@ -457,8 +560,8 @@ extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba,
   VQA_ARG(x && wa && wb && y && B > 0 && T > 0, "resblock_fwd: bad arguments");
   VQA_REQUIRE(vqa_resblock_supported(C, dilation, dtype), VQA_E_UNSUPPORTED,
               "resblock_fwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
-  VQA_ARG((long long)B * T * C < (1ll << 40), "resblock_fwd: tensor too large");
-  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0};
+  VQA_ARG((long long)T * C * 4 < (1ll << 30), "resblock_fwd: item too long for 32-bit buffer offsets (T=%d)", T);
+  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0, 0};
   plan(a, 3);
   const int esz = dtype == VQA_BF16 ? 2 : 4;
   const size_t lds = fwd_lds(RMAXD, esz);  // one LDS reservation for every dilation
@@ -489,12 +592,18 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
                                 vqa_partials_desc* desc, vqa_stream_t stream) {
   (void)bb;
   VQA_ARG(dy && x && wa && wb && dx && dwa && dwb && B > 0 && T > 0, "resblock_bwd: bad arguments");
+  VQA_ARG((long long)T * C * 4 < (1ll << 30), "resblock_bwd: item too long for 32-bit buffer offsets (T=%d)", T);
   VQA_REQUIRE(vqa_resblock_supported(C, dilation, dtype), VQA_E_UNSUPPORTED,
               "resblock_bwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
   const size_t need = vqa_resblock_bwd_workspace(B, T, C, dilation, dtype);
   VQA_ARG(workspace && ws_bytes >= need, "resblock_bwd: workspace %zu < %zu bytes", ws_bytes, need);
   const int E = 3 * RC * RC + RC;
-  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0};
+  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0};
+  static const int dbg_skip = [] {
+    const char* e = getenv("VQA_RESBLOCK_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  a.skip = dbg_skip;
   plan(a, kResPerCU);
   const int nwg = (a.ntiles + a.tpw - 1) / a.tpw;
   a.part_b = a.part_a + (size_t)nwg * E;
