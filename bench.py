@@ -8,10 +8,11 @@ codebook EMA with dead-code reset), replayed from a hipGraph. N > 1: data parall
 RCCL all_reduce of [grads | EMA sums | reset rows | losses] per step.
 
 Prints ONE JSON line on rank 0. Also reports:
-  roofline     — the dominant kernel's algorithmic bytes / its average duration: its launches of one step
-                 are recorded after the timed region and timed back to back in hipGraphs with HIP events
-                 on the stream it runs on; `traffic` = HBM bytes per launch from profiles/pmc_traffic.json
-                 (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) when present;
+  roofline     — the dominant kernel (fused residual-block backward) — its algorithmic bytes (SURVEY §8d layer
+                 model) / its average duration: its launches of one step are recorded after the timed region
+                 and timed back to back in hipGraphs with HIP events on the stream it runs on; `traffic` =
+                 HBM bytes per launch from profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE,
+                 gfx950 correction) when present; compulsory_* = the 3 tensors the fused kernel must move;
   cpu_baseline — the oracle (torch-CPU fp32 restatement of the reference op sequence) timed on the host
                  cores on a bounded sample (rank 0, N = 1 only).
 """
@@ -35,7 +36,7 @@ METRIC = "audio-samples/sec/GPU VQ-VAE train step, 44.1kHz 65536-frame chunks @1
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CFG2 = dict(levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2], num_embeddings=2048,
             residual_width=32, residual_depth=4, dilation_factor=3)
-DOMINANT = "conv32_kernel<bf16, C=32, O=32, TM=128>"  # 32-channel convs: forwards + fused data/weight gradients
+DOMINANT = "resblock_bwd_kernel<bf16>"  # fused residual-block backward (h recomputed): 104 launches per step
 
 
 def parse():
@@ -55,78 +56,52 @@ def parse():
     return p.parse_args()
 
 
-def gather_shape(op, C_in, C_out, stride):
-    """(gather C, gather O) of a conv entry point — mirrors the dispatch in csrc/vqa_conv.hip."""
-    if op == "conv1d_fwd":
-        return C_in, C_out
-    if op == "conv1d_bwd_data":
-        return (C_out, C_in) if stride == 1 else (C_out, 2 * C_in)
-    if op == "conv1d_transpose_fwd":
-        return C_in, 2 * C_out
-    return C_out, C_in  # conv1d_transpose_bwd_data
-
-
 class KernelTimer:
-    """Roofline of the dominant kernel, conv32_kernel<bf16> (C=32, O=32, TM=128): record every conv
-    launch of one step that dispatches to it (with its algorithmic bytes: gather input + output +
-    residual + mask, activation dtype), then time each distinct launch as back-to-back copies inside
-    a hipGraph replayed on the stream libvqa launches on, bracketed by HIP events (no host gaps, so the
-    per-launch average is the kernel's own duration, as rocprofv3 reports it)."""
+    """Roofline of the dominant kernel, resblock_bwd_kernel<bf16> (resnet.py:7-29 backward, one launch per
+    residual block): record every vqa_resblock_bwd call of one step, then time each distinct call as
+    back-to-back copies inside a hipGraph replayed on the stream libvqa launches on, bracketed by HIP events
+    (no host gaps, so the per-launch average is the kernel's own duration, as rocprofv3 reports it). The
+    weight-gradient partial reduction is left out (its own kernel).
 
-    OPS = ("conv1d_fwd", "conv1d_bwd_data", "conv1d_transpose_fwd", "conv1d_transpose_bwd_data",
-           "conv1d_bwd_data_weight")
+    Algorithmic bytes per launch (SURVEY.md §8d layer model): the launch does the data- and
+    weight-gradient of the block's two convs, 2 x (|in| + |out|) per conv = 8 activation tensors of
+    B*T*32 elements. Compulsory bytes (what the fused kernel must move: dy, x read, dx written) = 3."""
 
     def __init__(self, V):
         self.V = V
         self.calls = {}
-        self.orig = {}
-
-    def _dominant(self, op, args):
-        V = self.V
-        if op == "conv1d_bwd_data_weight":  # (dy, w, x, residual, dx, dw, db, B, T_in, T_out, C_in, C_out, K, s, ...)
-            C_in, C_out, stride, flags, dtype = args[10], args[11], args[13], args[16], args[17]
-            op = "conv1d_bwd_data"
-        else:
-            C_in, C_out, stride, flags, dtype = args[8], args[9], args[11], args[-2], args[-1]
-        if dtype != V.BF16 or flags & (V.X_F32 | V.Y_F32):
-            return False
-        return gather_shape(op, C_in, C_out, stride) == (32, 32)
+        self.orig = None
 
     def __enter__(self):
-        for op in self.OPS:
-            self.orig[op] = f = getattr(self.V, op)
+        self.orig = f = self.V.resblock_bwd
 
-            def wrapped(*args, _op=op, _f=f):
-                if self._dominant(_op, args):
-                    key = (_op,) + tuple(v for v in args if isinstance(v, int))
-                    if key in self.calls:
-                        self.calls[key][1] += 1
-                    else:  # algorithmic bytes: gather input, output, residual, mask / conv input
-                        ts = [t for t in args[:5] if isinstance(t, torch.Tensor) and t.numel() > 4096]
-                        self.calls[key] = [args, 1, sum(t.numel() * t.element_size() for t in ts)]
-                return _f(*args)
-            setattr(self.V, op, wrapped)
+        def wrapped(dy, x, *rest, _f=f):
+            key = (tuple(x.shape), x.dtype, rest[-2] if len(rest) >= 2 else None, x.data_ptr())
+            unit = x.numel() * x.element_size()
+            if key in self.calls:
+                self.calls[key][1] += 1
+            else:
+                self.calls[key] = [(dy, x) + tuple(rest), 1, 8 * unit, 3 * unit]
+            return _f(dy, x, *rest)
+        self.V.resblock_bwd = wrapped
         return self
 
     def __exit__(self, *a):
-        for op, f in self.orig.items():
-            setattr(self.V, op, f)
+        self.V.resblock_bwd = self.orig
 
     def measure(self, reps=5):
-        """-> (launches per step, total us per step, algorithmic bytes per step). Each distinct launch is
-        replayed as many times per graph as it occurs in a step, so these replays have the step's mix and
-        rocprofv3's average over the whole run stays comparable with avg_launch_us."""
-        n_launch, us_total, nbytes = 0, 0.0, 0
+        """-> (launches per step, total us per step, algorithmic bytes per step, compulsory bytes per step).
+        Each distinct launch is replayed as many times per graph as it occurs in a step, so the replays
+        have the step's mix and rocprofv3's average over the whole run stays comparable."""
+        n_launch, us_total, nbytes, cbytes = 0, 0.0, 0, 0
         stream = torch.cuda.current_stream()
-        for key, (args, cnt, nb) in self.calls.items():
-            f = self.orig[key[0]]
-            if key[0] == "conv1d_bwd_data_weight":  # time the kernel alone: leave the partials unreduced
-                f = (lambda *a, _f=f: _f(*a[:-1], self.V.Deferred()))
-            per_graph = cnt
+        f = self.orig
+        for key, (args, cnt, nb, cb) in self.calls.items():
+            args = args[:-1] + (self.V.Deferred(),)  # partials left unreduced: time the kernel alone
             f(*args)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for _ in range(per_graph):
+                for _ in range(cnt):
                     f(*args)
             g.replay()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -135,11 +110,12 @@ class KernelTimer:
                 g.replay()
             e.record(stream)
             torch.cuda.synchronize()
-            us = s.elapsed_time(e) * 1e3 / (reps * per_graph)
+            us = s.elapsed_time(e) * 1e3 / (reps * cnt)
             n_launch += cnt
             us_total += cnt * us
             nbytes += cnt * nb
-        return n_launch, us_total, nbytes
+            cbytes += cnt * cb
+        return n_launch, us_total, nbytes, cbytes
 
 
 def cpu_baseline(batch, steps, seq):
@@ -206,8 +182,9 @@ def main():
     with KernelTimer(V) as kt:
         model._compute(batches[0], True)
     torch.cuda.synchronize()
-    n_launch, us_total, nbytes = (0, 0.0, 0) if a.no_roofline else kt.measure()
+    n_launch, us_total, nbytes, cbytes = (0, 0.0, 0, 0) if a.no_roofline else kt.measure()
     achieved = nbytes / (us_total * 1e-6) / 1e9 if us_total > 0 else 0.0
+    compulsory = cbytes / (us_total * 1e-6) / 1e9 if us_total > 0 else 0.0
     traffic = None
     if os.path.exists(a.pmc_json):
         try:
@@ -218,6 +195,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": DOMINANT,
             "launches_per_step": n_launch, "avg_launch_us": round(us_total / max(n_launch, 1), 2),
             "algorithmic_bytes_per_launch": int(nbytes / max(n_launch, 1)),
+            "compulsory_bytes_per_launch": int(cbytes / max(n_launch, 1)),
+            "compulsory_GBps": round(compulsory, 1),
             "kernel_ms_per_step": round(us_total / 1e3, 3)}
 
     out = None

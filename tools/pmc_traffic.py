@@ -15,7 +15,7 @@ import os
 import re
 import sys
 
-FAMILY = re.compile(r"conv32_kernel(IDF16b|<__bf16)")
+FAMILY = re.compile(r"resblock_bwd_kernel(IDF16b|<__bf16|<bf16)")
 
 
 def per_dispatch(d, counter):
@@ -41,7 +41,7 @@ def main():
         raise SystemExit("no dispatches of the dominant kernel found")
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
-    res = {"kernel": "conv32_kernel<bf16, C=32, O=32, TM=128>",
+    res = {"kernel": "resblock_bwd_kernel<bf16>",
            "dispatches": [len(fetch), len(write)],
            "fetch_size_kib_per_launch": round(f_kib, 1), "write_size_kib_per_launch": round(w_kib, 1),
            "per_launch_bytes": int(2 * f_kib * 1024 + w_kib * 1024),

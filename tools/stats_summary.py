@@ -8,7 +8,7 @@ import json
 import re
 import sys
 
-FAMILY = re.compile(r"conv32_kernel(IDF16b|<__bf16)")
+FAMILY = re.compile(r"resblock_bwd_kernel(IDF16b|<__bf16|<bf16)")
 rows = list(csv.DictReader(open(sys.argv[1])))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"# rocprofv3 --kernel-trace --stats summary ({sys.argv[1].split('/')[-1]})\n")
@@ -20,7 +20,7 @@ for r in rows[:20]:
 fam = [r for r in rows if FAMILY.search(r["Name"])]
 calls = sum(int(r["Calls"]) for r in fam)
 dur = sum(float(r["TotalDurationNs"]) for r in fam)
-print(f"\nDominant kernel family conv32_kernel<bf16, C=32, O=32, TM=128> ({len(fam)} instantiations): "
+print(f"\nDominant kernel resblock_bwd_kernel<bf16> ({len(fam)} instantiations): "
       f"{calls} calls, average {dur / max(calls, 1) / 1e3:.2f} us, {100 * dur / tot:.1f} % of kernel time.")
 if len(sys.argv) > 2:
     b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
