@@ -6,15 +6,16 @@
 //   vqvae.py:309-326     _multispectral_loss = mean_b mean_res norm(S_x - S_r) / norm(S_x)
 // and the GradientTape backward of that expression w.r.t. the reconstruction (vqvae.py:143).
 //
-// One workgroup owns one STFT frame at a time (persistent loop over frames): the windowed target and
-// reconstruction frames are transformed by an in-LDS radix-4 Stockham FFT (fp32, twiddles from fp64
-// sincospi), the per-bin magnitudes |X_k|, |R_k| give the frame's partial sums sum (|X|-|R|)^2 and sum |X|^2,
-// and — for the gradient — the bin gradient G_k = (|R_k| - |X_k|) R_k / |R_k| (0 where |R_k| = 0, TF's
-// abs'(0)) is mapped back to the time domain by the adjoint of the one-sided rfft (an inverse FFT of the
-// Hermitian extension of G), windowed, and written unscaled per frame. The per-item scale
-// 1 / (nres * B * ||S_x - S_r|| * ||S_x||) is known only after every frame of the item is done, so a second
-// kernel reduces the partial sums per (item, resolution) and a third overlap-adds the frame gradients
-// (fixed summation order: deterministic) and applies the scales. No atomics, no host sync, graph-capturable.
+// A workgroup holds 256/TPF STFT frames at a time (TPF = N/4 threads per frame, at most 256), persistent
+// over the frames: the windowed target and reconstruction frames are transformed by an in-LDS radix-4
+// Stockham FFT (fp32; twiddles and window evaluated once per call in fp64 by spec_tables_kernel), the
+// per-bin magnitudes |X_k|, |R_k| give the frame's partial sums sum (|X|-|R|)^2 and sum |X|^2, and — for the
+// gradient — the bin gradient G_k = (|R_k| - |X_k|) R_k / |R_k| (0 where |R_k| = 0, TF's abs'(0)) is mapped
+// back to the time domain by the adjoint of the one-sided rfft (an inverse FFT of the Hermitian extension
+// of G), windowed, and written unscaled per frame. The per-item scale 1 / (nres * B * ||S_x - S_r|| *
+// ||S_x||) is known only after every frame of the item is done, so a second kernel reduces the partial sums
+// per (item, resolution) and a third overlap-adds the frame gradients (fixed summation order:
+// deterministic) and applies the scales. No atomics, no host sync, graph-capturable.
 #include "vqa_common.h"
 
 namespace vqa {
@@ -28,10 +29,11 @@ __device__ __forceinline__ f32x2 conj2(f32x2 a) { return f32x2{a.x, -a.y}; }
 __device__ __forceinline__ float cabs2(f32x2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
 
 // One radix-4 Stockham stage at stride S of an N-point transform: x -> y. tw[k] = exp(-2 pi i k / N).
-template <int N, int S, bool INV>
-__device__ __forceinline__ void fft_stage4(const f32x2* x, f32x2* y, const f32x2* tw) {
+// TPF threads (local id lt) work on one frame.
+template <int N, int S, bool INV, int TPF>
+__device__ __forceinline__ void fft_stage4(const f32x2* x, f32x2* y, const f32x2* tw, int lt) {
   constexpr int n = N / S, m = n / 4;
-  for (int j = threadIdx.x; j < N / 4; j += 256) {
+  for (int j = lt; j < N / 4; j += TPF) {
     const int p = j / S, q = j % S;
     const f32x2 a0 = x[q + S * p], a1 = x[q + S * (p + m)], a2 = x[q + S * (p + 2 * m)], a3 = x[q + S * (p + 3 * m)];
     f32x2 w1 = tw[p * S], w2 = tw[2 * p * S], w3 = tw[3 * p * S];
@@ -50,24 +52,24 @@ __device__ __forceinline__ void fft_stage4(const f32x2* x, f32x2* y, const f32x2
 }
 
 // the last stage when log2(N) is odd: n = 2, S = N/2
-template <int N>
-__device__ __forceinline__ void fft_stage2(const f32x2* x, f32x2* y) {
-  for (int q = threadIdx.x; q < N / 2; q += 256) {
+template <int N, int TPF>
+__device__ __forceinline__ void fft_stage2(const f32x2* x, f32x2* y, int lt) {
+  for (int q = lt; q < N / 2; q += TPF) {
     const f32x2 a = x[q], b = x[q + N / 2];
     y[q] = a + b;
     y[q + N / 2] = a - b;
   }
 }
 
-template <int N, int S, bool INV>
-__device__ __forceinline__ void fft_rec(f32x2* x, f32x2* y, const f32x2* tw) {
+template <int N, int S, bool INV, int TPF>
+__device__ __forceinline__ void fft_rec(f32x2* x, f32x2* y, const f32x2* tw, int lt) {
   constexpr int n = N / S;
   if constexpr (n >= 4) {
-    fft_stage4<N, S, INV>(x, y, tw);
+    fft_stage4<N, S, INV, TPF>(x, y, tw, lt);
     __syncthreads();
-    fft_rec<N, S * 4, INV>(y, x, tw);
+    fft_rec<N, S * 4, INV, TPF>(y, x, tw, lt);
   } else if constexpr (n == 2) {
-    fft_stage2<N>(x, y);
+    fft_stage2<N, TPF>(x, y, lt);
     __syncthreads();
   }
 }
@@ -81,79 +83,120 @@ template <int N> constexpr int fft_stages() {
   return s + (n == 2 ? 1 : 0);
 }
 
-// In-place (logically) N-point FFT of a[] in LDS; b[] is scratch. Returns the buffer holding the result
-// (natural order). Unnormalised in both directions. Caller syncs before (a written) — ends with a sync.
-template <int N, bool INV>
-__device__ __forceinline__ f32x2* fft(f32x2* a, f32x2* b, const f32x2* tw) {
-  fft_rec<N, 1, INV>(a, b, tw);
+// In-place (logically) N-point FFT of a[] in LDS; b[] is scratch. All frame slots of the workgroup run in
+// lockstep (workgroup barriers). Returns the buffer holding the result (natural order). Unnormalised in
+// both directions. Caller syncs before (a written) — ends with a sync.
+template <int N, bool INV, int TPF>
+__device__ __forceinline__ f32x2* fft(f32x2* a, f32x2* b, const f32x2* tw, int lt) {
+  fft_rec<N, 1, INV, TPF>(a, b, tw, lt);
   return (fft_stages<N>() & 1) ? b : a;
 }
 
 enum { SPEC_GRAD = 0, SPEC_LOSS = 1, SPEC_MAG = 2 };
+constexpr int SPEC_MAX_RES = 8;
 
 struct SpecFrameArgs {
-  const float* x;  // target (B, T) fp32
-  const float* r;  // reconstruction (B, T) fp32 (unused for SPEC_MAG)
-  float* fg;       // SPEC_GRAD: unscaled frame gradients (B*F, win)
-  float* part;     // SPEC_GRAD/LOSS: per-frame (sum (|X|-|R|)^2, sum |X|^2)
-  float* mag;      // SPEC_MAG: |X| (B*F, N/2+1)
+  const float* x;   // target (B, T) fp32
+  const float* r;   // reconstruction (B, T) fp32 (unused for SPEC_MAG)
+  float* fg;        // SPEC_GRAD: unscaled frame gradients (B*F, win)
+  float* part;      // SPEC_GRAD/LOSS: per-frame (sum (|X|-|R|)^2, sum |X|^2)
+  float* mag;       // SPEC_MAG: |X| (B*F, N/2+1)
+  const float* tw;  // N twiddles (re, im) from spec_tables_kernel, or null: evaluated in the kernel
+  const float* wn;  // periodic Hann window of length win (null with tw)
   int B, T, F, hop, win;
 };
 
+// threads per frame: N/4 butterflies per radix-4 stage, at most the whole workgroup
+template <int N> constexpr int spec_tpf() { return N / 4 < 256 ? N / 4 : 256; }
+
 template <int N, int MODE>
 __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
+  constexpr int TPF = spec_tpf<N>(), FPI = 256 / TPF;  // frame slots per workgroup
+  constexpr int KB = N / 2 + 1, NB = (KB + TPF - 1) / TPF, WPF = TPF / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  f32x2* buf0 = (f32x2*)smem;
-  f32x2* buf1 = buf0 + N;
-  f32x2* tw = buf1 + N;
+  f32x2* tw = (f32x2*)smem;
   float* wn = (float*)(tw + N);
-  constexpr int KB = N / 2 + 1, NB = (KB + 255) / 256;
-  const int tid = threadIdx.x;
+  f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
+  const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF, wave = tid >> 6;
+  f32x2* buf0 = slots + (size_t)sl * 2 * N;
+  f32x2* buf1 = buf0 + N;
+  __shared__ float red[2][4];
 
-  // twiddles exp(-2 pi i k / N) and the periodic Hann window (tf.signal.hann_window(win, periodic=True)),
-  // both evaluated in fp64 and rounded once
-  for (int k = tid; k < N; k += 256) {
-    double s, c;
-    sincospi(2.0 * (double)k / (double)N, &s, &c);
-    tw[k] = f32x2{(float)c, (float)-s};
+  if (a.tw) {
+    // tables computed once per call (fp64, rounded once): 16-byte copies
+    for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
+    for (int e = tid; e < a.win; e += 256) wn[e] = a.wn[e];
+  } else {
+    for (int k = tid; k < N; k += 256) {
+      double sn, cs;
+      sincospi(2.0 * (double)k / (double)N, &sn, &cs);
+      tw[k] = f32x2{(float)cs, (float)-sn};
+    }
+    for (int n = tid; n < a.win; n += 256) wn[n] = (float)(0.5 - 0.5 * cospi(2.0 * (double)n / (double)a.win));
   }
-  for (int n = tid; n < a.win; n += 256) wn[n] = (float)(0.5 - 0.5 * cospi(2.0 * (double)n / (double)a.win));
   __syncthreads();
 
-  __shared__ float red[4];
   const int nframes = a.B * a.F;
-  for (int fi = blockIdx.x; fi < nframes; fi += gridDim.x) {
-    const int bb = fi / a.F, f = fi - bb * a.F;
+  // the samples of a frame slot, NL per thread (n = lt + i*TPF), are loaded one frame ahead into registers
+  constexpr int NL = N / TPF;
+  float xv[NL], rv[NL];
+  auto load_frame = [&](int f0_) {
+    const int fc = min(f0_ + sl, nframes - 1);  // an idle slot recomputes a valid frame and stores nothing
+    const int bb = fc / a.F, f = fc - bb * a.F;
     const size_t off = (size_t)bb * a.T + (size_t)f * a.hop;
-    const float* xs = a.x + off;
-    for (int n = tid; n < N; n += 256) buf0[n] = n < a.win ? f32x2{xs[n] * wn[n], 0.f} : f32x2{0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int n = lt + i * TPF;
+      const int nc = n < a.win ? n : 0;
+      xv[i] = a.x[off + nc];
+      if constexpr (MODE != SPEC_MAG) rv[i] = a.r[off + nc];
+    }
+  };
+  if (blockIdx.x * FPI < nframes) load_frame(blockIdx.x * FPI);
+  for (int f0 = blockIdx.x * FPI; f0 < nframes; f0 += gridDim.x * FPI) {
+    const int fi = f0 + sl;
+    const bool act = fi < nframes;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int n = lt + i * TPF;
+      buf0[n] = n < a.win ? f32x2{xv[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
+    }
+    float rcur[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) rcur[i] = (MODE != SPEC_MAG) ? rv[i] : 0.f;
+    if (f0 + gridDim.x * FPI < nframes) load_frame(f0 + gridDim.x * FPI);  // lands during this frame's FFTs
     __syncthreads();
-    const f32x2* X = fft<N, false>(buf0, buf1, tw);
+    const f32x2* X = fft<N, false, TPF>(buf0, buf1, tw, lt);
     float mx[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int k = tid + 256 * j;
+      const int k = lt + TPF * j;
       mx[j] = k < KB ? cabs2(X[k]) : 0.f;
     }
     if constexpr (MODE == SPEC_MAG) {
+      if (act) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int k = tid + 256 * j;
-        if (k < KB) a.mag[(size_t)fi * KB + k] = mx[j];
+        for (int j = 0; j < NB; ++j) {
+          const int k = lt + TPF * j;
+          if (k < KB) a.mag[(size_t)fi * KB + k] = mx[j];
+        }
       }
       __syncthreads();
       continue;
     } else {
       __syncthreads();  // every read of X done before buf0/buf1 are reused
-      const float* rs = a.r + off;
-      for (int n = tid; n < N; n += 256) buf0[n] = n < a.win ? f32x2{rs[n] * wn[n], 0.f} : f32x2{0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int n = lt + i * TPF;
+        buf0[n] = n < a.win ? f32x2{rcur[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
+      }
       __syncthreads();
-      f32x2* R = fft<N, false>(buf0, buf1, tw);
+      f32x2* R = fft<N, false, TPF>(buf0, buf1, tw, lt);
       f32x2* H = (R == buf0) ? buf1 : buf0;  // free since the last FFT stage's sync
       float sd = 0.f, sx = 0.f;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const int k = tid + 256 * j;
+        const int k = lt + TPF * j;
         if (k < KB) {
           const f32x2 rk = R[k];
           const float mr = cabs2(rk), d = mx[j] - mr;
@@ -172,26 +215,58 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
           }
         }
       }
-      sd = block_sum_256(sd, red);
-      __syncthreads();
-      sx = block_sum_256(sx, red);
-      if (tid == 0) {
-        a.part[2 * (size_t)fi] = sd;
-        a.part[2 * (size_t)fi + 1] = sx;
+      // per-slot sums: wave sums, then the slot's waves in a fixed order
+      sd = warp_sum(sd);
+      sx = warp_sum(sx);
+      if ((tid & 63) == 0) {
+        red[0][wave] = sd;
+        red[1][wave] = sx;
+      }
+      __syncthreads();  // also orders the H writes before the inverse FFT
+      if (lt == 0 && act) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPF; ++w) {
+          s0 += red[0][sl * WPF + w];
+          s1 += red[1][sl * WPF + w];
+        }
+        a.part[2 * (size_t)fi] = s0;
+        a.part[2 * (size_t)fi + 1] = s1;
       }
       if constexpr (MODE == SPEC_GRAD) {
-        // block_sum_256's syncs ordered the H writes before this point
         f32x2* other = (H == buf0) ? buf1 : buf0;
-        const f32x2* Y = fft<N, true>(H, other, tw);
-        float* out = a.fg + (size_t)fi * a.win;
-        for (int n = tid; n < a.win; n += 256) out[n] = Y[n].x * wn[n];
+        const f32x2* Y = fft<N, true, TPF>(H, other, tw, lt);
+        if (act) {
+          float* out = a.fg + (size_t)fi * a.win;
+          for (int n = lt; n < a.win; n += TPF) out[n] = Y[n].x * wn[n];
+        }
       }
-      __syncthreads();
+      __syncthreads();  // red[] and the slot buffers are reused by the next frames
     }
   }
 }
 
-constexpr int SPEC_MAX_RES = 8;
+// twiddles exp(-2 pi i k / N) (N complex per resolution) and periodic Hann windows
+// (tf.signal.hann_window(win, periodic=True)), evaluated in fp64 and rounded once
+struct SpecTables {
+  float* tw[SPEC_MAX_RES];
+  float* wn[SPEC_MAX_RES];
+  int N[SPEC_MAX_RES], win[SPEC_MAX_RES];
+  int nres;
+};
+
+__global__ __launch_bounds__(256) void spec_tables_kernel(SpecTables t) {
+  const int res = blockIdx.y;
+  const int N = t.N[res], W = t.win[res];
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < N; k += gridDim.x * 256) {
+    double sn, cs;
+    sincospi(2.0 * (double)k / (double)N, &sn, &cs);
+    t.tw[res][2 * k] = (float)cs;
+    t.tw[res][2 * k + 1] = (float)-sn;
+  }
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < W; n += gridDim.x * 256)
+    t.wn[res][n] = (float)(0.5 - 0.5 * cospi(2.0 * (double)n / (double)W));
+}
 
 struct SpecScaleArgs {
   const float* part[SPEC_MAX_RES];
@@ -265,13 +340,18 @@ __global__ __launch_bounds__(256) void spec_gather_kernel(SpecGatherArgs a) {
 
 template <int N, int MODE>
 static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
-  const size_t lds = (size_t)3 * N * sizeof(f32x2) + (size_t)fa.win * sizeof(float);
+  constexpr int FPI = 256 / spec_tpf<N>();
+  const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((fa.win + 3) & ~3) * sizeof(float) +
+                     (size_t)FPI * 2 * N * sizeof(f32x2);
   const int nframes = fa.B * fa.F;
-  const int grid = nframes < 4096 ? nframes : 4096;
+  const int groups = (nframes + FPI - 1) / FPI;
+  const int grid = groups < 2048 ? groups : 2048;
   hipLaunchKernelGGL((spec_frame_kernel<N, MODE>), dim3(grid), dim3(256), lds, s, fa);
   VQA_LAUNCHED("spec_frame_kernel");
   return VQA_OK;
 }
+
+static bool spec_n_ok(int n) { return n == 256 || n == 512 || n == 1024 || n == 2048; }
 
 template <int MODE>
 static int dispatch_frames(int n_fft, const SpecFrameArgs& fa, hipStream_t s) {
@@ -286,22 +366,32 @@ static int dispatch_frames(int n_fft, const SpecFrameArgs& fa, hipStream_t s) {
 
 static size_t align64(size_t n) { return (n + 63) & ~(size_t)63; }
 
-// workspace layout (floats): per resolution [fg (grad only) | part], then [lossbr | scale]
+// workspace layout (floats): per resolution [fg (grad only) | part | twiddles (2N) | window], then
+// [lossbr | scale]
+struct SpecLayout {
+  size_t fg[SPEC_MAX_RES], part[SPEC_MAX_RES], tw[SPEC_MAX_RES], wn[SPEC_MAX_RES], tail, total;
+  int F[SPEC_MAX_RES];
+};
+
 static int spec_layout(int B, int T, const int* n_fft, const int* hop, const int* win, int nres, bool grad,
-                       size_t* fg_off, size_t* part_off, int* F, size_t* tail_off, size_t* total) {
+                       SpecLayout* L) {
   if (B <= 0 || T <= 0 || nres <= 0 || nres > SPEC_MAX_RES || !n_fft || !hop || !win) return VQA_E_INVALID_ARG;
   size_t o = 0;
   for (int r = 0; r < nres; ++r) {
     if (hop[r] <= 0 || win[r] <= 0 || win[r] > n_fft[r] || win[r] > T) return VQA_E_INVALID_ARG;
-    F[r] = 1 + (T - win[r]) / hop[r];
-    fg_off[r] = o;
-    if (grad) o += align64((size_t)B * F[r] * win[r]);
-    part_off[r] = o;
-    o += align64((size_t)B * F[r] * 2);
+    L->F[r] = 1 + (T - win[r]) / hop[r];
+    L->fg[r] = o;
+    if (grad) o += align64((size_t)B * L->F[r] * win[r]);
+    L->part[r] = o;
+    o += align64((size_t)B * L->F[r] * 2);
+    L->tw[r] = o;
+    o += align64((size_t)2 * n_fft[r]);
+    L->wn[r] = o;
+    o += align64((size_t)win[r]);
   }
-  *tail_off = o;
+  L->tail = o;
   o += align64((size_t)B * nres * 2);
-  *total = o * sizeof(float);
+  L->total = o * sizeof(float);
   return VQA_OK;
 }
 
@@ -311,10 +401,9 @@ using namespace vqa;
 
 extern "C" size_t vqa_spectral_loss_workspace(int B, int T, const int* n_fft, const int* hop, const int* win,
                                               int nres, int with_grad) {
-  size_t fo[SPEC_MAX_RES], po[SPEC_MAX_RES], tail, total;
-  int F[SPEC_MAX_RES];
-  if (spec_layout(B, T, n_fft, hop, win, nres, with_grad != 0, fo, po, F, &tail, &total) != VQA_OK) return 0;
-  return total;
+  SpecLayout L;
+  if (spec_layout(B, T, n_fft, hop, win, nres, with_grad != 0, &L) != VQA_OK) return 0;
+  return L.total;
 }
 
 extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out, float* dr, float* item_loss, int B,
@@ -322,28 +411,43 @@ extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out
                                  size_t ws_bytes, vqa_stream_t stream) {
   VQA_ARG(x && r && loss_out, "spectral_loss: null pointer");
   const bool grad = dr != nullptr;
-  size_t fo[SPEC_MAX_RES], po[SPEC_MAX_RES], tail, total;
-  int F[SPEC_MAX_RES];
-  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, grad, fo, po, F, &tail, &total) == VQA_OK,
+  SpecLayout L;
+  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, grad, &L) == VQA_OK,
           "spectral_loss: bad shape (B=%d T=%d nres=%d; need 0 < win <= n_fft, win <= T, hop > 0)", B, T, nres);
-  VQA_ARG(workspace && ws_bytes >= total, "spectral_loss: workspace %zu < %zu bytes", ws_bytes, total);
+  for (int i = 0; i < nres; ++i)
+    VQA_REQUIRE(spec_n_ok(n_fft[i]), VQA_E_UNSUPPORTED, "spectral: n_fft %d unsupported (256, 512, 1024, 2048)",
+                n_fft[i]);
+  VQA_ARG(workspace && ws_bytes >= L.total, "spectral_loss: workspace %zu < %zu bytes", ws_bytes, L.total);
   hipStream_t s = (hipStream_t)stream;
   float* ws = (float*)workspace;
+  SpecTables tb{};
+  int maxn = 0;
+  for (int i = 0; i < nres; ++i) {
+    tb.tw[i] = ws + L.tw[i];
+    tb.wn[i] = ws + L.wn[i];
+    tb.N[i] = n_fft[i];
+    tb.win[i] = win[i];
+    maxn = n_fft[i] > maxn ? n_fft[i] : maxn;
+  }
+  tb.nres = nres;
+  hipLaunchKernelGGL(spec_tables_kernel, dim3((maxn + 255) / 256, nres), dim3(256), 0, s, tb);
+  VQA_LAUNCHED("spec_tables_kernel");
   SpecScaleArgs sa{};
   SpecGatherArgs ga{};
   for (int i = 0; i < nres; ++i) {
-    SpecFrameArgs fa{x, r, ws + fo[i], ws + po[i], nullptr, B, T, F[i], hop[i], win[i]};
+    SpecFrameArgs fa{x, r, ws + L.fg[i], ws + L.part[i], nullptr, ws + L.tw[i], ws + L.wn[i], B, T, L.F[i], hop[i],
+                     win[i]};
     const int rc = grad ? dispatch_frames<SPEC_GRAD>(n_fft[i], fa, s) : dispatch_frames<SPEC_LOSS>(n_fft[i], fa, s);
     if (rc != VQA_OK) return rc;
-    sa.part[i] = ws + po[i];
-    sa.F[i] = F[i];
-    ga.fg[i] = ws + fo[i];
-    ga.F[i] = F[i];
+    sa.part[i] = ws + L.part[i];
+    sa.F[i] = L.F[i];
+    ga.fg[i] = ws + L.fg[i];
+    ga.F[i] = L.F[i];
     ga.hop[i] = hop[i];
     ga.win[i] = win[i];
   }
-  sa.lossbr = ws + tail;
-  sa.scale = ws + tail + (size_t)B * nres;
+  sa.lossbr = ws + L.tail;
+  sa.scale = ws + L.tail + (size_t)B * nres;
   sa.nres = nres;
   sa.inv = (float)(1.0 / ((double)nres * (double)B));
   hipLaunchKernelGGL(spec_scale_kernel, dim3(B * nres), dim3(256), 0, s, sa);
@@ -368,6 +472,7 @@ extern "C" int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int 
   VQA_ARG(x && mag && B > 0 && hop > 0 && win > 0 && win <= n_fft && win <= T,
           "stft_magnitude: bad arguments (B=%d T=%d n_fft=%d hop=%d win=%d)", B, T, n_fft, hop, win);
   const int F = 1 + (T - win) / hop;
-  SpecFrameArgs fa{x, nullptr, nullptr, nullptr, mag, B, T, F, hop, win};
+  // no workspace in this entry point: the kernel evaluates its twiddles and window itself
+  SpecFrameArgs fa{x, nullptr, nullptr, nullptr, mag, nullptr, nullptr, B, T, F, hop, win};
   return dispatch_frames<SPEC_MAG>(n_fft, fa, (hipStream_t)stream);
 }
