@@ -209,6 +209,18 @@ int vqa_spectral_loss(const float* x, const float* r, float* loss_out, float* dr
                       vqa_stream_t stream);
 size_t vqa_spectral_loss_workspace(int B, int T, const int* n_fft, const int* hop, const int* win, int nres,
                                    int with_grad);
+/* The same loss in two parts, for a target shared by several reconstructions (the levels of one train
+ * step): vqa_spectral_target writes the FFT tables and |S_x| of every resolution into `target`
+ * (vqa_spectral_target_workspace bytes); vqa_spectral_loss_target then takes that buffer instead of x
+ * (workspace: vqa_spectral_loss_target_workspace). vqa_spectral_loss = both in one call. */
+size_t vqa_spectral_target_workspace(int B, int T, const int* n_fft, const int* hop, const int* win, int nres);
+int vqa_spectral_target(const float* x, void* target, size_t target_bytes, int B, int T, const int* n_fft,
+                        const int* hop, const int* win, int nres, vqa_stream_t stream);
+size_t vqa_spectral_loss_target_workspace(int B, int T, const int* n_fft, const int* hop, const int* win, int nres,
+                                          int with_grad);
+int vqa_spectral_loss_target(const void* target, const float* r, float* loss_out, float* dr, float* item_loss, int B,
+                             int T, const int* n_fft, const int* hop, const int* win, int nres, void* workspace,
+                             size_t ws_bytes, vqa_stream_t stream);
 /* data_utils.py:25-30 spectral(x) for one resolution: mag (B, F, n_fft/2 + 1) fp32 = |tf.signal.stft(x)|. */
 int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int n_fft, int hop, int win, vqa_stream_t stream);
 

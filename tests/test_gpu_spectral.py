@@ -97,3 +97,25 @@ def test_bad_shapes(cuda):
         V.spectral_loss_workspace(2, 1000, *STFT_ARGS)  # 1000 < win 1200
     with pytest.raises(V.VQAError):
         V.stft_magnitude(x, torch.empty(1, device=cuda), 4096, 10, 100)  # n_fft unsupported
+
+
+@pytest.mark.parametrize("B,T", [(3, 4096 + 113), (2, 65536)])
+def test_shared_target(cuda, B, T):
+    """One vqa_spectral_target buffer serves several reconstructions (the levels of a train step) and gives
+    the same bits as the one-call vqa_spectral_loss; odd frame counts exercise the unpaired last frame."""
+    x, r = _signals(B, T, seed=11 + T)
+    tgt = SpectralTarget(x.to(cuda))
+    for k, scale in enumerate((0.3, 0.05)):
+        rr = (scale * torch.randn(B, T, 1, generator=torch.Generator().manual_seed(k)) + 0.5 * x).to(cuda)
+        l1, g1 = multispectral_loss_and_grad(tgt, rr)
+        l0 = torch.empty(1, device=cuda)
+        g0 = torch.empty(B, T, device=cuda)
+        V.spectral_loss(tgt.x, rr.reshape(B, T), l0, g0, None, *STFT_ARGS)
+        assert torch.equal(l0, l1) and torch.equal(g0, g1.reshape(B, T))
+        l2, _ = multispectral_loss_and_grad(tgt, rr, need_grad=False)
+        assert torch.equal(l1, l2)
+    if T < 10000:
+        loss_ref, _, g_ref = _oracle(x, rr.cpu())
+        assert abs(float(l1) - loss_ref) / loss_ref < 1e-5
+        err = (g1.cpu().double() - g_ref).abs().max() / g_ref.abs().max()
+        assert err < 1e-4, err

@@ -246,6 +246,151 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
   }
 }
 
+// Loss (and gradient) of the reconstruction against PRECOMPUTED target magnitudes |S_x| (the target's STFT
+// is the same for every level of a step, so it is transformed once, by spec_frame_kernel<SPEC_MAG>). A frame
+// slot takes frames in PAIRS (a, b): two forward FFTs of the windowed reconstruction frames, then ONE inverse
+// FFT of H_a + i H_b — both adjoint outputs are real, so y_a = Re, y_b = Im exactly (no cancellation: the
+// forward transforms stay separate). 1.5 FFTs per frame instead of 3.
+struct SpecPairArgs {
+  const float* r;   // reconstruction (B, T) fp32
+  const float* tm;  // target magnitudes (B*F, N/2+1)
+  float* fg;        // GRAD: unscaled frame gradients (B*F, win)
+  float* part;      // per-frame (sum (|X|-|R|)^2, sum |X|^2)
+  const float* tw;  // N twiddles (re, im)
+  const float* wn;  // window
+  int B, T, F, hop, win;
+};
+
+template <int N, bool GRAD>
+__global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
+  constexpr int TPF = spec_tpf<N>(), FPI = 256 / TPF;  // frame-pair slots per workgroup
+  constexpr int KB = N / 2 + 1, NB = (KB + TPF - 1) / TPF, WPF = TPF / 64, NL = N / TPF;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  f32x2* tw = (f32x2*)smem;
+  float* wn = (float*)(tw + N);
+  f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
+  const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF, wave = tid >> 6;
+  f32x2* bA = slots + (size_t)sl * 3 * N;
+  f32x2* bB = bA + N;
+  f32x2* bC = bB + N;
+  __shared__ float red[4][4];
+
+  for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
+  for (int e = tid; e < a.win; e += 256) wn[e] = a.wn[e];
+  __syncthreads();
+
+  const int nframes = a.B * a.F, npairs = (nframes + 1) / 2;
+  // samples and target magnitudes of the slot's pair, loaded one pair ahead into registers
+  float ra[NL], rb[NL], ta[NB], tb[NB];
+  auto load_pair = [&](int p0) {
+    const int pa = min(2 * (p0 + sl), nframes - 1), pb = min(2 * (p0 + sl) + 1, nframes - 1);
+    const int ba_ = pa / a.F, bb_ = pb / a.F;
+    const size_t oa = (size_t)ba_ * a.T + (size_t)(pa - ba_ * a.F) * a.hop;
+    const size_t ob = (size_t)bb_ * a.T + (size_t)(pb - bb_ * a.F) * a.hop;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int n = lt + i * TPF, nc = n < a.win ? n : 0;
+      ra[i] = a.r[oa + nc];
+      rb[i] = a.r[ob + nc];
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int k = lt + TPF * j, kc = k < KB ? k : 0;
+      ta[j] = a.tm[(size_t)pa * KB + kc];
+      tb[j] = a.tm[(size_t)pb * KB + kc];
+    }
+  };
+  if (blockIdx.x * FPI < npairs) load_pair(blockIdx.x * FPI);
+  for (int p0 = blockIdx.x * FPI; p0 < npairs; p0 += gridDim.x * FPI) {
+    const int fa = 2 * (p0 + sl), fb = fa + 1;
+    const bool acta = fa < nframes, actb = fb < nframes;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int n = lt + i * TPF;
+      const bool in = n < a.win;
+      bA[n] = in ? f32x2{ra[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
+      bB[n] = in ? f32x2{rb[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
+    }
+    float mxa[NB], mxb[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      mxa[j] = ta[j];
+      mxb[j] = tb[j];
+    }
+    if (p0 + gridDim.x * FPI < npairs) load_pair(p0 + gridDim.x * FPI);  // lands during this pair's FFTs
+    __syncthreads();
+    f32x2* Ra = fft<N, false, TPF>(bA, bC, tw, lt);
+    f32x2* sc = (Ra == bA) ? bC : bA;
+    f32x2* Rb = fft<N, false, TPF>(bB, sc, tw, lt);
+    // the buffer holding neither spectrum receives H
+    f32x2* H = (Ra != bA && Rb != bA) ? bA : ((Ra != bB && Rb != bB) ? bB : bC);
+    float sda = 0.f, sxa = 0.f, sdb = 0.f, sxb = 0.f;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int k = lt + TPF * j;
+      if (k < KB) {
+        const f32x2 rka = Ra[k], rkb = Rb[k];
+        const float mra = cabs2(rka), mrb = cabs2(rkb);
+        const float da = mxa[j] - mra, db = mxb[j] - mrb;
+        sda += da * da;
+        sxa += mxa[j] * mxa[j];
+        sdb += db * db;
+        sxb += mxb[j] * mxb[j];
+        if constexpr (GRAD) {
+          // dL/d(Re,Im)R_k = (|R|-|X|) R/|R| (0 at |R| = 0); H = H_a + i H_b, each the Hermitian extension
+          // of G/2 (G at k = 0, N/2)
+          const float ga = mra > 0.f ? (mra - mxa[j]) / mra : 0.f;
+          const float gb = mrb > 0.f ? (mrb - mxb[j]) / mrb : 0.f;
+          const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
+          if (k == 0 || k == N / 2) {
+            H[k] = f32x2{Ga.x, Gb.x};
+          } else {
+            H[k] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
+            H[N - k] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
+          }
+        }
+      }
+    }
+    sda = warp_sum(sda);
+    sxa = warp_sum(sxa);
+    sdb = warp_sum(sdb);
+    sxb = warp_sum(sxb);
+    if ((tid & 63) == 0) {
+      red[0][wave] = sda;
+      red[1][wave] = sxa;
+      red[2][wave] = sdb;
+      red[3][wave] = sxb;
+    }
+    __syncthreads();  // also orders the H writes before the inverse FFT
+    if (lt == 0) {
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < WPF; ++w)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) s[v] += red[v][sl * WPF + w];
+      if (acta) {
+        a.part[2 * (size_t)fa] = s[0];
+        a.part[2 * (size_t)fa + 1] = s[1];
+      }
+      if (actb) {
+        a.part[2 * (size_t)fb] = s[2];
+        a.part[2 * (size_t)fb + 1] = s[3];
+      }
+    }
+    if constexpr (GRAD) {
+      const f32x2* Y = fft<N, true, TPF>(H, Ra, tw, lt);  // Ra's spectrum is no longer read
+      float* oa = a.fg + (size_t)fa * a.win;
+      float* ob = a.fg + (size_t)fb * a.win;
+      for (int n = lt; n < a.win; n += TPF) {
+        const f32x2 y = Y[n];
+        if (acta) oa[n] = y.x * wn[n];
+        if (actb) ob[n] = y.y * wn[n];
+      }
+    }
+    __syncthreads();  // red[] and the slot buffers are reused by the next pair
+  }
+}
+
 // twiddles exp(-2 pi i k / N) (N complex per resolution) and periodic Hann windows
 // (tf.signal.hann_window(win, periodic=True)), evaluated in fp64 and rounded once
 struct SpecTables {
@@ -364,12 +509,47 @@ static int dispatch_frames(int n_fft, const SpecFrameArgs& fa, hipStream_t s) {
   }
 }
 
+template <int N, bool GRAD>
+static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
+  constexpr int FPI = 256 / spec_tpf<N>();
+  const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((pa.win + 3) & ~3) * sizeof(float) +
+                     (size_t)FPI * 3 * N * sizeof(f32x2);
+  static size_t lds_set = 0;
+  if (lds > 65536 && lds > lds_set) {
+    if (hipFuncSetAttribute((const void*)spec_pair_kernel<N, GRAD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("spectral: cannot reserve %zu B of LDS", lds);
+      return VQA_E_UNSUPPORTED;
+    }
+    lds_set = lds;
+  }
+  const int npairs = (pa.B * pa.F + 1) / 2;
+  const int groups = (npairs + FPI - 1) / FPI;
+  const int grid = groups < 2048 ? groups : 2048;
+  hipLaunchKernelGGL((spec_pair_kernel<N, GRAD>), dim3(grid), dim3(256), lds, s, pa);
+  VQA_LAUNCHED("spec_pair_kernel");
+  return VQA_OK;
+}
+
+template <bool GRAD>
+static int dispatch_pairs(int n_fft, const SpecPairArgs& pa, hipStream_t s) {
+  switch (n_fft) {
+    case 256: return launch_pairs<256, GRAD>(pa, s);
+    case 512: return launch_pairs<512, GRAD>(pa, s);
+    case 1024: return launch_pairs<1024, GRAD>(pa, s);
+    case 2048: return launch_pairs<2048, GRAD>(pa, s);
+    default: set_error("spectral: n_fft %d unsupported (256, 512, 1024, 2048)", n_fft); return VQA_E_UNSUPPORTED;
+  }
+}
+
 static size_t align64(size_t n) { return (n + 63) & ~(size_t)63; }
 
-// workspace layout (floats): per resolution [fg (grad only) | part | twiddles (2N) | window], then
-// [lossbr | scale]
+// Target region (floats; per resolution: twiddles 2N | window | |S_x| (B*F, N/2+1)) and loss workspace
+// (per resolution: frame gradients (grad only) | per-frame partials; then per-item losses | scales).
 struct SpecLayout {
-  size_t fg[SPEC_MAX_RES], part[SPEC_MAX_RES], tw[SPEC_MAX_RES], wn[SPEC_MAX_RES], tail, total;
+  size_t tw[SPEC_MAX_RES], wn[SPEC_MAX_RES], tm[SPEC_MAX_RES], target;
+  size_t fg[SPEC_MAX_RES], part[SPEC_MAX_RES], tail, loss;
   int F[SPEC_MAX_RES];
 };
 
@@ -378,53 +558,36 @@ static int spec_layout(int B, int T, const int* n_fft, const int* hop, const int
   if (B <= 0 || T <= 0 || nres <= 0 || nres > SPEC_MAX_RES || !n_fft || !hop || !win) return VQA_E_INVALID_ARG;
   size_t o = 0;
   for (int r = 0; r < nres; ++r) {
-    if (hop[r] <= 0 || win[r] <= 0 || win[r] > n_fft[r] || win[r] > T) return VQA_E_INVALID_ARG;
+    if (hop[r] <= 0 || win[r] <= 0 || win[r] > n_fft[r] || win[r] > T || !spec_n_ok(n_fft[r])) return VQA_E_INVALID_ARG;
     L->F[r] = 1 + (T - win[r]) / hop[r];
-    L->fg[r] = o;
-    if (grad) o += align64((size_t)B * L->F[r] * win[r]);
-    L->part[r] = o;
-    o += align64((size_t)B * L->F[r] * 2);
     L->tw[r] = o;
     o += align64((size_t)2 * n_fft[r]);
     L->wn[r] = o;
     o += align64((size_t)win[r]);
+    L->tm[r] = o;
+    o += align64((size_t)B * L->F[r] * (n_fft[r] / 2 + 1));
+  }
+  L->target = o * sizeof(float);
+  o = 0;
+  for (int r = 0; r < nres; ++r) {
+    L->fg[r] = o;
+    if (grad) o += align64((size_t)B * L->F[r] * win[r]);
+    L->part[r] = o;
+    o += align64((size_t)B * L->F[r] * 2);
   }
   L->tail = o;
   o += align64((size_t)B * nres * 2);
-  L->total = o * sizeof(float);
+  L->loss = o * sizeof(float);
   return VQA_OK;
 }
 
-}  // namespace vqa
-
-using namespace vqa;
-
-extern "C" size_t vqa_spectral_loss_workspace(int B, int T, const int* n_fft, const int* hop, const int* win,
-                                              int nres, int with_grad) {
-  SpecLayout L;
-  if (spec_layout(B, T, n_fft, hop, win, nres, with_grad != 0, &L) != VQA_OK) return 0;
-  return L.total;
-}
-
-extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out, float* dr, float* item_loss, int B,
-                                 int T, const int* n_fft, const int* hop, const int* win, int nres, void* workspace,
-                                 size_t ws_bytes, vqa_stream_t stream) {
-  VQA_ARG(x && r && loss_out, "spectral_loss: null pointer");
-  const bool grad = dr != nullptr;
-  SpecLayout L;
-  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, grad, &L) == VQA_OK,
-          "spectral_loss: bad shape (B=%d T=%d nres=%d; need 0 < win <= n_fft, win <= T, hop > 0)", B, T, nres);
-  for (int i = 0; i < nres; ++i)
-    VQA_REQUIRE(spec_n_ok(n_fft[i]), VQA_E_UNSUPPORTED, "spectral: n_fft %d unsupported (256, 512, 1024, 2048)",
-                n_fft[i]);
-  VQA_ARG(workspace && ws_bytes >= L.total, "spectral_loss: workspace %zu < %zu bytes", ws_bytes, L.total);
-  hipStream_t s = (hipStream_t)stream;
-  float* ws = (float*)workspace;
+static int spec_target(const float* x, float* tg, const SpecLayout& L, int B, int T, const int* n_fft, const int* hop,
+                       const int* win, int nres, hipStream_t s) {
   SpecTables tb{};
   int maxn = 0;
   for (int i = 0; i < nres; ++i) {
-    tb.tw[i] = ws + L.tw[i];
-    tb.wn[i] = ws + L.wn[i];
+    tb.tw[i] = tg + L.tw[i];
+    tb.wn[i] = tg + L.wn[i];
     tb.N[i] = n_fft[i];
     tb.win[i] = win[i];
     maxn = n_fft[i] > maxn ? n_fft[i] : maxn;
@@ -432,12 +595,24 @@ extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out
   tb.nres = nres;
   hipLaunchKernelGGL(spec_tables_kernel, dim3((maxn + 255) / 256, nres), dim3(256), 0, s, tb);
   VQA_LAUNCHED("spec_tables_kernel");
+  for (int i = 0; i < nres; ++i) {
+    SpecFrameArgs fa{x, nullptr, nullptr, nullptr, tg + L.tm[i], tg + L.tw[i], tg + L.wn[i], B, T, L.F[i], hop[i],
+                     win[i]};
+    if (int rc = dispatch_frames<SPEC_MAG>(n_fft[i], fa, s)) return rc;
+  }
+  return VQA_OK;
+}
+
+static int spec_loss(const float* tg, const float* r, float* loss_out, float* dr, float* item_loss, float* ws,
+                     const SpecLayout& L, int B, int T, const int* n_fft, const int* hop, const int* win, int nres,
+                     hipStream_t s) {
+  const bool grad = dr != nullptr;
   SpecScaleArgs sa{};
   SpecGatherArgs ga{};
   for (int i = 0; i < nres; ++i) {
-    SpecFrameArgs fa{x, r, ws + L.fg[i], ws + L.part[i], nullptr, ws + L.tw[i], ws + L.wn[i], B, T, L.F[i], hop[i],
-                     win[i]};
-    const int rc = grad ? dispatch_frames<SPEC_GRAD>(n_fft[i], fa, s) : dispatch_frames<SPEC_LOSS>(n_fft[i], fa, s);
+    SpecPairArgs pa{r, tg + L.tm[i], ws + L.fg[i], ws + L.part[i], tg + L.tw[i], tg + L.wn[i], B, T, L.F[i], hop[i],
+                    win[i]};
+    const int rc = grad ? dispatch_pairs<true>(n_fft[i], pa, s) : dispatch_pairs<false>(n_fft[i], pa, s);
     if (rc != VQA_OK) return rc;
     sa.part[i] = ws + L.part[i];
     sa.F[i] = L.F[i];
@@ -465,6 +640,67 @@ extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out
   hipLaunchKernelGGL(spec_gather_kernel, dim3((int)nb), dim3(256), 0, s, ga);
   VQA_LAUNCHED("spec_gather_kernel");
   return VQA_OK;
+}
+
+}  // namespace vqa
+
+using namespace vqa;
+
+#define SPEC_SHAPE_ERR "spectral: bad shape (B=%d T=%d nres=%d; need 0 < win <= n_fft, win <= T, hop > 0, " \
+                       "n_fft in {256, 512, 1024, 2048})"
+
+extern "C" size_t vqa_spectral_target_workspace(int B, int T, const int* n_fft, const int* hop, const int* win,
+                                                int nres) {
+  SpecLayout L;
+  return spec_layout(B, T, n_fft, hop, win, nres, false, &L) == VQA_OK ? L.target : 0;
+}
+
+extern "C" int vqa_spectral_target(const float* x, void* target, size_t target_bytes, int B, int T, const int* n_fft,
+                                   const int* hop, const int* win, int nres, vqa_stream_t stream) {
+  VQA_ARG(x && target, "spectral_target: null pointer");
+  SpecLayout L;
+  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, false, &L) == VQA_OK, SPEC_SHAPE_ERR, B, T, nres);
+  VQA_ARG(target_bytes >= L.target, "spectral_target: buffer %zu < %zu bytes", target_bytes, L.target);
+  return spec_target(x, (float*)target, L, B, T, n_fft, hop, win, nres, (hipStream_t)stream);
+}
+
+extern "C" size_t vqa_spectral_loss_target_workspace(int B, int T, const int* n_fft, const int* hop, const int* win,
+                                                     int nres, int with_grad) {
+  SpecLayout L;
+  return spec_layout(B, T, n_fft, hop, win, nres, with_grad != 0, &L) == VQA_OK ? L.loss : 0;
+}
+
+extern "C" int vqa_spectral_loss_target(const void* target, const float* r, float* loss_out, float* dr,
+                                        float* item_loss, int B, int T, const int* n_fft, const int* hop,
+                                        const int* win, int nres, void* workspace, size_t ws_bytes,
+                                        vqa_stream_t stream) {
+  VQA_ARG(target && r && loss_out, "spectral_loss_target: null pointer");
+  SpecLayout L;
+  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, dr != nullptr, &L) == VQA_OK, SPEC_SHAPE_ERR, B, T, nres);
+  VQA_ARG(workspace && ws_bytes >= L.loss, "spectral_loss_target: workspace %zu < %zu bytes", ws_bytes, L.loss);
+  return spec_loss((const float*)target, r, loss_out, dr, item_loss, (float*)workspace, L, B, T, n_fft, hop, win, nres,
+                   (hipStream_t)stream);
+}
+
+extern "C" size_t vqa_spectral_loss_workspace(int B, int T, const int* n_fft, const int* hop, const int* win,
+                                              int nres, int with_grad) {
+  SpecLayout L;
+  if (spec_layout(B, T, n_fft, hop, win, nres, with_grad != 0, &L) != VQA_OK) return 0;
+  return L.target + L.loss;
+}
+
+extern "C" int vqa_spectral_loss(const float* x, const float* r, float* loss_out, float* dr, float* item_loss, int B,
+                                 int T, const int* n_fft, const int* hop, const int* win, int nres, void* workspace,
+                                 size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(x && r && loss_out, "spectral_loss: null pointer");
+  SpecLayout L;
+  VQA_ARG(spec_layout(B, T, n_fft, hop, win, nres, dr != nullptr, &L) == VQA_OK, SPEC_SHAPE_ERR, B, T, nres);
+  VQA_ARG(workspace && ws_bytes >= L.target + L.loss, "spectral_loss: workspace %zu < %zu bytes", ws_bytes,
+          L.target + L.loss);
+  hipStream_t s = (hipStream_t)stream;
+  float* tg = (float*)workspace;
+  if (int rc = spec_target(x, tg, L, B, T, n_fft, hop, win, nres, s)) return rc;
+  return spec_loss(tg, r, loss_out, dr, item_loss, tg + L.target / sizeof(float), L, B, T, n_fft, hop, win, nres, s);
 }
 
 extern "C" int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int n_fft, int hop, int win,

@@ -42,30 +42,34 @@ def norm(x: torch.Tensor) -> torch.Tensor:
 
 
 class SpectralTarget:
-    """The target waveform of one batch, (B, T) fp32 on the device. The spectral kernel re-derives |S_x| per
-    frame in LDS next to |S_r| (cheaper than storing and re-reading the target spectrogram per level)."""
+    """The target waveform of one batch, (B, T) fp32 on the device, and its spectrograms |S_x| for every
+    resolution (computed once by vqa_spectral_target and shared by the loss of every level)."""
 
     def __init__(self, x: torch.Tensor):
         self.x = x.reshape(x.shape[0], -1).float().contiguous()
         self.B, self.T = self.x.shape
+        self.mags = V.spectral_target(self.x, *STFT_ARGS)
         self._ws = {}
 
     def workspace(self, grad: bool) -> torch.Tensor:
         if grad not in self._ws:
-            n = V.spectral_loss_workspace(self.B, self.T, *STFT_ARGS, with_grad=grad)
+            n = V.spectral_loss_target_workspace(self.B, self.T, *STFT_ARGS, with_grad=grad)
             self._ws[grad] = V.workspace(n, self.x.device)
         return self._ws[grad]
 
 
 def multispectral_loss_and_grad(target: SpectralTarget, recon: torch.Tensor, loss_out=None, need_grad=True):
     """vqvae.py:309-326 _multispectral_loss (mean over the batch of the per-item mean over resolutions) and
-    its gradient d loss / d recon, (B, T, 1) fp32 — one vqa_spectral_loss call. Returns (loss (1,), grad)."""
+    its gradient d loss / d recon, (B, T, 1) fp32 — one vqa_spectral_loss_target call against the shared
+    target spectrograms. Returns (loss (1,), grad)."""
     r = recon.reshape(recon.shape[0], -1)
     if r.dtype != torch.float32:
         raise ValueError("the multispectral loss takes the fp32 reconstruction")
+    if r.shape != target.x.shape:
+        raise ValueError(f"reconstruction {tuple(r.shape)} vs target {tuple(target.x.shape)}")
     loss = loss_out if loss_out is not None else torch.empty(1, dtype=torch.float32, device=r.device)
     dr = torch.empty_like(r) if need_grad else None
-    V.spectral_loss(target.x, r.contiguous(), loss, dr, None, *STFT_ARGS, ws=target.workspace(need_grad))
+    V.spectral_loss_target(target.mags, r.contiguous(), loss, dr, None, *STFT_ARGS, ws=target.workspace(need_grad))
     return loss, (dr.reshape(recon.shape) if need_grad else None)
 
 

@@ -31,6 +31,8 @@ EXPORTED = [
     "vqa_spectral_loss", "vqa_spectral_loss_workspace", "vqa_stft_magnitude",
     "vqa_vq_argmin_split", "vqa_vq_split_bf16x3",
     "vqa_resblock_supported", "vqa_resblock_fwd", "vqa_resblock_bwd", "vqa_resblock_bwd_workspace",
+    "vqa_spectral_target_workspace", "vqa_spectral_target", "vqa_spectral_loss_target_workspace",
+    "vqa_spectral_loss_target",
 ]
 
 
@@ -88,6 +90,10 @@ _SIGS = {
     "vqa_resblock_fwd": (_I, [_P] * 7 + [_I] * 5 + [_P]),
     "vqa_resblock_bwd": (_I, [_P] * 11 + [_I] * 5 + [_P, _S, _P, _P]),
     "vqa_resblock_bwd_workspace": (_S, [_I] * 5),
+    "vqa_spectral_target_workspace": (_S, [_I, _I, _P, _P, _P, _I]),
+    "vqa_spectral_target": (_I, [_P, _P, _S, _I, _I, _P, _P, _P, _I, _P]),
+    "vqa_spectral_loss_target_workspace": (_S, [_I, _I, _P, _P, _P, _I, _I]),
+    "vqa_spectral_loss_target": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _S, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -369,6 +375,37 @@ def spectral_loss(x, r, loss_out, dr, item_loss, n_fft, hop, win, ws=None):
     _check(lib().vqa_spectral_loss(ptr(x), ptr(r), ptr(loss_out), ptr(dr), ptr(item_loss), B, T, _int_array(n_fft),
                                    _int_array(hop), _int_array(win), nres, ptr(ws), ws.numel(), stream()),
            "vqa_spectral_loss")
+
+
+def spectral_target(x, n_fft, hop, win):
+    """Tables + |S_x| of every resolution for a (B, T) fp32 target -> a uint8 device buffer."""
+    B, T = x.shape[0], x.numel() // x.shape[0]
+    a = (_int_array(n_fft), _int_array(hop), _int_array(win))
+    n = lib().vqa_spectral_target_workspace(B, T, *a, len(n_fft))
+    if n == 0:
+        raise VQAError(f"spectral_target: bad shape B={B} T={T} n_fft={n_fft} hop={hop} win={win}")
+    tg = workspace(n, x.device)
+    _check(lib().vqa_spectral_target(ptr(x), ptr(tg), tg.numel(), B, T, *a, len(n_fft), stream()),
+           "vqa_spectral_target")
+    return tg
+
+
+def spectral_loss_target_workspace(B, T, n_fft, hop, win, with_grad=True) -> int:
+    n = lib().vqa_spectral_loss_target_workspace(B, T, _int_array(n_fft), _int_array(hop), _int_array(win),
+                                                 len(n_fft), 1 if with_grad else 0)
+    if n == 0:
+        raise VQAError(f"spectral_loss_target: bad shape B={B} T={T} n_fft={n_fft} hop={hop} win={win}")
+    return n
+
+
+def spectral_loss_target(target, r, loss_out, dr, item_loss, n_fft, hop, win, ws=None):
+    """The spectral loss of r (B, T) against a spectral_target buffer; dr / item_loss may be None."""
+    B, T = r.shape[0], r.numel() // r.shape[0]
+    a = (_int_array(n_fft), _int_array(hop), _int_array(win))
+    if ws is None:
+        ws = workspace(spectral_loss_target_workspace(B, T, n_fft, hop, win, dr is not None), r.device)
+    _check(lib().vqa_spectral_loss_target(ptr(target), ptr(r), ptr(loss_out), ptr(dr), ptr(item_loss), B, T, *a,
+                                          len(n_fft), ptr(ws), ws.numel(), stream()), "vqa_spectral_loss_target")
 
 
 def stft_magnitude(x, mag, n_fft, hop, win):
