@@ -46,21 +46,116 @@ struct ResArgs {
 template <class T> constexpr int rs_stride() { return RC + lds_pad<T>(); }
 constexpr int round16(int v) { return (v + 15) & ~15; }
 
-// weights -> LDS image [3][32][WS]: TRANSPOSE=true gives [k][o][c] (A operand of a forward conv),
-// false the Keras layout [k][c][o] (A operand of the transposed conv)
+// ---------------------------------------------------------------------------------------------------
+// Lane maps. Every tile lives in LDS as [row][32 channels] at an 80-byte row stride (bf16). The maps below
+// choose which lane handles which row / channel so that the kernels' LDS instructions are free of bank
+// conflicts (MI355X_MICROARCH.md "LDS": ds_read_b128 serves lane groups {0-3,12-15,20-27}, ... on 64
+// banks, ds_write_b128 groups of 8 contiguous lanes on 32 banks, ds_read_b64_tr_b16 32-lane halves):
+//   rs_pi(n)   tile row of MFMA column n = lane & 15: {0-3, 12-15} -> the odd rows, {4-11} -> the even rows
+//   rs_sig(g)  16-byte channel chunk of lane group g = lane >> 4: 0, 2, 1, 3. Used for the 8 output
+//              channels a lane holds after an MFMA pair (row m of output tile mt = channel
+//              8 sig(m >> 2) + 4 mt + (m & 3)), and — KPERM, backward only — for the K slice of the bf16
+//              A/B fragments. Without KPERM every output is the same MFMA sum in the same K order as the
+//              unfused gather kernels (the forward stays bit-identical to them).
+//   rs_rows    the transposed (K = rows) fragment of the weight-gradient products takes its 32 rows as
+//              even rows in lanes 0-31 and odd rows in lanes 32-63 (same K map for both operands).
+__device__ __forceinline__ int rs_pi(int n) {
+  return 2 * ((n & 3) | ((n >> 1) & 4)) + (((n >> 3) ^ (n >> 2) ^ 1) & 1);
+}
+__device__ __forceinline__ int rs_sig(int g) { return ((g & 1) << 1) | (g >> 1); }
+template <class T, bool KPERM> __device__ __forceinline__ int rs_kcol(int lane) {
+  if constexpr (sizeof(T) == 2) return 8 * (KPERM ? rs_sig(lane >> 4) : (lane >> 4));
+  else return lane >> 4;
+}
+// first of the 8 consecutive output channels a lane holds after the MFMAs of tiles mt = 0, 1
+__device__ __forceinline__ int rs_ocol(int lane) { return 8 * rs_sig(lane >> 4); }
+// A-operand row (within one tap's 32 rows) that produces output channel oc
+__device__ __forceinline__ int rs_arow(int oc) { return ((oc >> 2) & 1) * 16 + rs_pi(4 * rs_sig(oc >> 3) + (oc & 3)); }
+
+template <class T> __device__ __forceinline__ typename Mfma<T>::frag rs_rows(const T* o, int stride);
+template <> __device__ __forceinline__ bf16x8 rs_rows<bf16>(const bf16* o, int stride) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const bf16* a0 = o + (2 * (4 * (g & 1) + (i >> 2)) + (g >> 1)) * stride + 4 * (i & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 16 * stride));
+  return __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+template <> __device__ __forceinline__ float rs_rows<float>(const float* o, int stride) {
+  return Mfma<float>::rows(o, stride);
+}
+
+// the lane's 8 consecutive channels (lo: tile mt = 0, hi: mt = 1) <-> memory (one 16-byte access for bf16)
+template <class T> __device__ __forceinline__ void ld8(const T* p, f32x4& lo, f32x4& hi);
+template <> __device__ __forceinline__ void ld8<float>(const float* p, f32x4& lo, f32x4& hi) {
+  lo = *(const f32x4*)p;
+  hi = *(const f32x4*)(p + 4);
+}
+template <> __device__ __forceinline__ void ld8<bf16>(const bf16* p, f32x4& lo, f32x4& hi) {
+  const bf16x8 v = *(const bf16x8*)p;
+  lo = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  hi = f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+}
+template <class T> __device__ __forceinline__ void st8(T* p, f32x4 lo, f32x4 hi);
+template <> __device__ __forceinline__ void st8<float>(float* p, f32x4 lo, f32x4 hi) {
+  *(f32x4*)p = lo;
+  *(f32x4*)(p + 4) = hi;
+}
+template <> __device__ __forceinline__ void st8<bf16>(bf16* p, f32x4 lo, f32x4 hi) {
+  const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
+                    (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+  *(bf16x8*)p = o;
+}
+
+// store of the lane's 8 channels through a buffer descriptor: rows past the item's end are dropped by the
+// hardware range check (no per-lane branch)
+template <class T>
+__device__ __forceinline__ void st8_buf(__amdgpu_buffer_rsrc_t r, int byte_off, f32x4 lo, f32x4 hi) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
+                      (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), r, byte_off, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, lo), r, byte_off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, hi), r, byte_off + 16, 0, 0);
+  }
+}
+
+// (value > 0) for the lane's 8 channels read from LDS (bf16: signed 16-bit compares on the raw bits, so
+// -0 counts as not positive)
+template <class T> __device__ __forceinline__ void pos8(const T* p, bool (&m)[8]);
+template <> __device__ __forceinline__ void pos8<bf16>(const bf16* p, bool (&m)[8]) {
+  const uint4 u = *(const uint4*)p;
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    m[2 * i] = (short)(w[i] & 0xFFFFu) > 0;
+    m[2 * i + 1] = (int)w[i] > 0xFFFF;
+  }
+}
+template <> __device__ __forceinline__ void pos8<float>(const float* p, bool (&m)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = p[i] > 0.f;
+}
+
+// weights -> LDS image [3][32][WS] of A operands: image row k*32 + rs_arow(oc) holds the weights of the
+// conv's output channel oc over its input channels (natural order). TRANSPOSE=true: a forward conv
+// (output = Keras o, input = c); false: the transposed conv (output = c, input = o).
 template <class T, bool TRANSPOSE>
 __device__ __forceinline__ void stage_wimg(T* img, const float* w) {
   constexpr int WS = rs_stride<T>();
   for (int e = threadIdx.x; e < 3 * RC * RC; e += 256) {
-    const int k = e / (RC * RC), rem = e - k * RC * RC, r = rem / RC, c = rem - r * RC;
     // e enumerates the Keras layout: w[k][r][c] with r = input channel, c = output channel
-    if (TRANSPOSE) img[(k * RC + c) * WS + r] = (T)w[e];
-    else img[(k * RC + r) * WS + c] = (T)w[e];
+    const int k = e / (RC * RC), rem = e - k * RC * RC, r = rem / RC, c = rem - r * RC;
+    const int oc = TRANSPOSE ? c : r, ic = TRANSPOSE ? r : c;
+    img[(k * RC + rs_arow(oc)) * WS + ic] = (T)w[e];
   }
 }
 
-// The same through a per-item buffer descriptor: the hardware range check returns zeros for rows outside
-// [0, T) (SAME padding; negative offsets wrap past num_records), so a chunk costs one add and one
+// The tile loads go through a per-item buffer descriptor: the hardware range check returns zeros for rows
+// outside [0, T) (SAME padding; negative offsets wrap past num_records), so a chunk costs one add and one
 // buffer_load, and the per-thread chunk offsets are fixed for the launch.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs_rsrc(const void* base, unsigned bytes) {
   const unsigned long long p = (unsigned long long)base;
@@ -71,6 +166,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs_rsrc(const void* base, unsi
 }
 constexpr int kRsOOB = -0x40000000;  // chunk offset that stays out of range for any row base
 
+// Rows of a tile staged HBM -> registers -> LDS, 16 B per chunk. bf16 rows are 4 chunks; the 8 contiguous
+// lanes of one ds_write_b128 bank group take rows r and r + 4 (disjoint 16-dword windows at 80-byte rows).
 template <class T, int PV>
 struct Rows32Buf {
   static constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC, ROWB = RC * (int)sizeof(T);
@@ -81,8 +178,16 @@ struct Rows32Buf {
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const int e = threadIdx.x + i * 256;
-      const int rr = e / CPR, q = e - rr * CPR;
-      const bool in = e < nrows * CPR;
+      int rr, q;
+      if constexpr (CPR == 4) {
+        const int G = e >> 3;
+        rr = 8 * (G >> 2) + (G & 3) + 4 * ((e >> 2) & 1);
+        q = e & 3;
+      } else {
+        rr = e / CPR;
+        q = e - rr * CPR;
+      }
+      const bool in = rr < nrows;
       goff[i] = in ? rr * ROWB + q * 16 : kRsOOB;
       loff[i] = in ? rr * XS + q * VEC : -1;
     }
@@ -93,96 +198,59 @@ struct Rows32Buf {
     for (int i = 0; i < PV; ++i)
       v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, goff[i] + base, 0, 0));
   }
+  template <bool RELU>
   __device__ __forceinline__ void store(T* dst) const {
 #pragma unroll
     for (int i = 0; i < PV; ++i)
-      if (loff[i] >= 0) *(uint4*)(dst + loff[i]) = v[i];
+      if (loff[i] >= 0) {
+        uint4 w = v[i];
+        if constexpr (RELU) {
+          if constexpr (sizeof(T) == 2) w = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, w)));
+          else relu_bits<T>(w);
+        }
+        *(uint4*)(dst + loff[i]) = w;
+      }
   }
 };
 
 // chunks per thread for the largest tile of a launch (rows <= 256 at RMAXD)
 template <class T> constexpr int rs_pv() { return sizeof(T) == 2 ? 4 : 8; }
 
-// acc[mt] (16 output channels each) for 16 output rows: out[row][o] = sum_k sum_c img[k][o][c] *
-// act(in[row_base + k*tap_step + row][c]); lane: row = lane & 15, channels mt*16 + 4*(lane>>4) + 0..3.
-// Tap order k = 0, 1, 2 then channel blocks — the accumulation order of the unfused gather kernels.
-template <class T, bool RELU_IN>
-__device__ __forceinline__ void conv_rows16(f32x4 (&acc)[2], const T* img, const T* in, int row_base, int tap_step) {
-  typedef Mfma<T> M;
-  constexpr int WS = rs_stride<T>(), XS = rs_stride<T>();
-  const int lane = threadIdx.x & 63, ko = M::koff(lane);
-  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const T* wk = img + (k * RC + (lane & 15)) * WS + ko;
-    const T* xr = in + (row_base + k * tap_step + (lane & 15)) * XS + ko;
-#pragma unroll
-    for (int cc = 0; cc < RC; cc += M::KS) {
-      const typename M::frag a0 = M::load(wk + cc), a1 = M::load(wk + 16 * WS + cc);
-      typename M::frag b = M::load(xr + cc);
-      if (RELU_IN) b = relu_frag(b);
-      acc[0] = M::mma(a0, b, acc[0]);
-      acc[1] = M::mma(a1, b, acc[1]);
-    }
-  }
-}
-
-// The same with the weights held in registers: wf[k][mt][cc-step] = A fragments of a forward conv
-// (A[m = o][K = c] = W[k][c][o], Keras layout), loaded once per workgroup by load_wfrags.
 template <class T> constexpr int rs_ncc() { return RC / Mfma<T>::KS; }
 
+// A fragments of a forward conv held in registers: wf[k][mt][cc-step] (A[m][K] = W[k][c][och(mt, m)],
+// Keras layout), loaded once per workgroup
 template <class T>
 __device__ __forceinline__ void load_wfrags(typename Mfma<T>::frag (&wf)[3][2][rs_ncc<T>()], const float* w) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, m = lane & 15, kc = rs_kcol<T, false>(lane);
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int s = 0; s < rs_ncc<T>(); ++s) {
-        const int o = mt * 16 + (lane & 15);
+        const int o = 8 * rs_sig(m >> 2) + 4 * mt + (m & 3);
         if constexpr (sizeof(T) == 2) {
-          const int c0 = s * 32 + 8 * (lane >> 4);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) wf[k][mt][s][j] = (bf16)w[(k * RC + c0 + j) * RC + o];
+          for (int j = 0; j < 8; ++j) wf[k][mt][s][j] = (bf16)w[(k * RC + s * 32 + kc + j) * RC + o];
         } else {
-          wf[k][mt][s] = w[(k * RC + s * 4 + (lane >> 4)) * RC + o];
+          wf[k][mt][s] = w[(k * RC + s * 4 + kc) * RC + o];
         }
       }
 }
 
-template <class T, bool RELU_IN>
-__device__ __forceinline__ void conv_rows16r(f32x4 (&acc)[2], const typename Mfma<T>::frag (&wf)[3][2][rs_ncc<T>()],
-                                             const T* in, int row_base, int tap_step) {
-  typedef Mfma<T> M;
-  constexpr int XS = rs_stride<T>();
-  const int lane = threadIdx.x & 63, ko = M::koff(lane);
-  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const T* xr = in + (row_base + k * tap_step + (lane & 15)) * XS + ko;
-#pragma unroll
-    for (int s = 0; s < rs_ncc<T>(); ++s) {
-      typename M::frag b = M::load(xr + s * M::KS);
-      if (RELU_IN) b = relu_frag(b);
-      acc[0] = M::mma(wf[k][0][s], b, acc[0]);
-      acc[1] = M::mma(wf[k][1][s], b, acc[1]);
-    }
-  }
-}
-
 // NJ 16-row n-tiles at once: every B fragment is loaded before the first MFMA, then the MFMAs run tap-major
 // over the n-tiles (2*NJ independent accumulator chains), so the LDS latency and the MFMA dependency chain
-// are hidden inside the wave. afrag(k, mt, s) supplies the A fragment (registers or an LDS image). Same
-// accumulation order per output as conv_rows16.
-template <class T, bool RELU_IN, int NJ, class AFrag>
+// are hidden inside the wave. Output acc[j][mt]: rows rb[j] + rs_pi(lane & 15), channels rs_ocol(lane) +
+// 4 mt + 0..3. afrag(k, mt, s) supplies the A fragment (registers or an LDS image). Tap order k = 0, 1, 2,
+// then channel blocks — the accumulation order of the unfused gather kernels.
+template <class T, bool RELU_IN, bool KPERM, bool ALDS, int NJ, class AFrag>
 __device__ __forceinline__ void conv_multi(f32x4 (&acc)[NJ][2], AFrag afrag, const T* in, const int (&rb)[NJ],
                                            int tap_step) {
   typedef Mfma<T> M;
   constexpr int XS = rs_stride<T>(), NCC = rs_ncc<T>();
-  const int lane = threadIdx.x & 63, ko = M::koff(lane);
+  const int lane = threadIdx.x & 63;
+  const T* base = in + rs_pi(lane & 15) * XS + rs_kcol<T, KPERM>(lane);
   typename M::frag b[NJ][3][NCC];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
@@ -190,7 +258,7 @@ __device__ __forceinline__ void conv_multi(f32x4 (&acc)[NJ][2], AFrag afrag, con
     for (int k = 0; k < 3; ++k)
 #pragma unroll
       for (int s = 0; s < NCC; ++s) {
-        b[j][k][s] = M::load(in + (rb[j] + k * tap_step + (lane & 15)) * XS + ko + s * M::KS);
+        b[j][k][s] = M::load(base + (rb[j] + k * tap_step) * XS + s * M::KS);
         if (RELU_IN) b[j][k][s] = relu_frag(b[j][k][s]);
       }
 #pragma unroll
@@ -198,17 +266,29 @@ __device__ __forceinline__ void conv_multi(f32x4 (&acc)[NJ][2], AFrag afrag, con
     acc[j][0] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  typename M::frag af[3][NCC][2];
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
     for (int s = 0; s < NCC; ++s) {
-      const typename M::frag a0 = afrag(k, 0, s), a1 = afrag(k, 1, s);
+      af[k][s][0] = afrag(k, 0, s);
+      af[k][s][1] = afrag(k, 1, s);
+    }
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int s = 0; s < NCC; ++s)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        acc[j][0] = M::mma(a0, b[j][k][s], acc[j][0]);
-        acc[j][1] = M::mma(a1, b[j][k][s], acc[j][1]);
+        acc[j][0] = M::mma(af[k][s][0], b[j][k][s], acc[j][0]);
+        acc[j][1] = M::mma(af[k][s][1], b[j][k][s], acc[j][1]);
       }
-    }
+  if constexpr (sizeof(T) == 2) {
+    // issue order: every LDS fragment read (B and, from an image, A), then the MFMAs — the reads overlap
+    // each other instead of one read -> wait -> MFMA pair at a time
+    __builtin_amdgcn_sched_group_barrier(0x100, NJ * 3 * NCC + (ALDS ? 6 * NCC : 0), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, NJ * 6 * NCC, 0);
+  }
 }
 
 __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o], b[o + 1], b[o + 2], b[o + 3]}; }
@@ -217,27 +297,26 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o
 // 3 waves/SIMD for bf16 (<= 168 VGPRs without spilling); the fp32 parity build needs more registers
 template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2; }
 
-template <class T>
+template <class T, int DT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_fwd_waves<T>(), 8)))
 void resblock_fwd_kernel(ResArgs a) {
-  typedef Mfma<T> M;
   constexpr int XS = rs_stride<T>(), HR = RTM + 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* X = (T*)smem;  // local j <-> row t0 - 1 - d + j, XR = HR + 2d rows (raw x)
-  const int d = a.d, XR = HR + 2 * d;
+  const int d = DT > 0 ? DT : a.d, XR = HR + 2 * d;
   T* H = X + XR * XS;  // local i <-> row t0 - 1 + i, relu(h)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
   if (tbeg >= tend) return;
-  typename M::frag wfa[3][2][rs_ncc<T>()], wfb[3][2][rs_ncc<T>()];
+  typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()], wfb[3][2][rs_ncc<T>()];
   load_wfrags<T>(wfa, a.wa);
   load_wfrags<T>(wfb, a.wb);
+  const int pn = rs_pi(lane & 15), oc = rs_ocol(lane);
   f32x4 bav[2], bbv[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
-    const int o = mt * 16 + 4 * (lane >> 4);
-    bav[mt] = a.ba ? bias4(a.ba, o) : f32x4{0.f, 0.f, 0.f, 0.f};
-    bbv[mt] = a.bb ? bias4(a.bb, o) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bav[mt] = a.ba ? bias4(a.ba, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bbv[mt] = a.bb ? bias4(a.bb, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
   auto item_x = [&](int tile) { return rs_rsrc((const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC, ibytes); };
@@ -245,7 +324,7 @@ void resblock_fwd_kernel(ResArgs a) {
   Rows32Buf<T, rs_pv<T>()> nx;
   nx.init(XR);
   nx.load(item_x(tbeg), row0(tbeg));
-  nx.store(X);
+  nx.template store<false>(X);
   if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1));
   __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
@@ -260,53 +339,49 @@ void resblock_fwd_kernel(ResArgs a) {
       f32x4 acc[3][2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = min(wave + 4 * j, HR / 16 - 1) * 16;
-      conv_multi<T, true, 3>(acc, wa_frag, X, rb, d);
+      conv_multi<T, true, false, false, 3>(acc, wa_frag, X, rb, d);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= HR / 16) continue;
-        const int i = rb[j] + (lane & 15), r = t0 - 1 + i;
+        const int i = rb[j] + pn, r = t0 - 1 + i;
         const bool live = interior || (r >= 0 && r < a.T);
-        const bool own = a.h && live && i >= 1 && i <= RTM;
+        f32x4 v[2];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          f32x4 v = acc[j][mt] + bav[mt];
+          v[mt] = acc[j][mt] + bav[mt];
           if (interior) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+            for (int q = 0; q < 4; ++q) v[mt][q] = fmaxf(v[mt][q], 0.f);
           } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
+            for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
-          st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
-          if (own) st4((T*)a.h + ((size_t)n * a.T + r) * RC + mt * 16 + 4 * (lane >> 4), v);
         }
+        st8(H + i * XS + oc, v[0], v[1]);
+        // the tile's own rows 1..RTM (rows >= T dropped by the range check)
+        if (a.h && i >= 1 && i <= RTM)
+          st8_buf<T>(rs_rsrc((T*)a.h + (size_t)n * a.T * RC, ibytes), (r * RC + oc) * (int)sizeof(T), v[0], v[1]);
       }
     }
     __syncthreads();
-    T* yi = (T*)a.y + (size_t)n * a.T * RC;
     {
+      const __amdgpu_buffer_rsrc_t yr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
       int rb[2];
       f32x4 acc[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16;
-      conv_multi<T, false, 2>(acc, wb_frag, H, rb, 1);
+      conv_multi<T, false, false, false, 2>(acc, wb_frag, H, rb, 1);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int tl = rb[j] + (lane & 15), t = t0 + tl;
-        if (t < a.T) {
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) {
-            const int o = mt * 16 + 4 * (lane >> 4);
-            f32x4 v = acc[j][mt] + bbv[mt];
-            v = ld4(X + (tl + 1 + d) * XS + o) + v;
-            st4(yi + (size_t)t * RC + o, v);
-          }
-        }
+        const int tl = rb[j] + pn;
+        f32x4 x0, x1;
+        ld8(X + (tl + 1 + d) * XS + oc, x0, x1);
+        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + (acc[j][0] + bbv[0]), x1 + (acc[j][1] + bbv[1]));
       }
     }
     if (tile + 1 < tend) {
       __syncthreads();  // every read of X and H for this tile is done
-      nx.store(X);
+      nx.template store<false>(X);
       if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2));
       __syncthreads();
     }
@@ -314,27 +389,30 @@ void resblock_fwd_kernel(ResArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-template <class T>
+// DT > 0: the dilation as a compile-time constant (every LDS offset of the tile becomes an immediate);
+// DT = 0: any dilation <= RMAXD from the arguments
+template <class T, int DT>
 __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
   constexpr int WS = rs_stride<T>(), XS = WS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int d = a.d, HR = round16(RTM + 2 * d), XR = HR + 2 * d, YR = HR + 2;
-  T* waF = (T*)smem;            // conv_a forward (recompute h): [k][o][c]
-  T* waT = waF + 3 * RC * WS;   // conv_a^T: Keras [k][c][o]
-  T* wbT = waT + 3 * RC * WS;   // conv_b^T: Keras [k][c][o]
-  T* X = wbT + 3 * RC * WS;     // local j <-> row t0 - 2d + j (raw x)
+  const int d = DT > 0 ? DT : a.d, HR = round16(RTM + 2 * d), XR = HR + 2 * d, YR = HR + 2;
+  T* waF = (T*)smem;            // conv_a forward (recompute h): output o, input c
+  T* waT = waF + 3 * RC * WS;   // conv_a^T: output c, input o
+  T* wbT = waT + 3 * RC * WS;   // conv_b^T: output c, input o
+  T* X = wbT + 3 * RC * WS;     // local j <-> row t0 - 2d + j: relu(x)
   T* Y = X + XR * XS;           // local m <-> row t0 - d - 1 + m (dy)
   T* H = Y + YR * XS;           // local i <-> row t0 - d + i: relu(h), then dh
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
   if (tbeg >= tend) return;
   stage_wimg<T, true>(waF, a.wa);
   stage_wimg<T, false>(waT, a.wa);
   stage_wimg<T, false>(wbT, a.wb);
+  const int pn = rs_pi(lane & 15), oc = rs_ocol(lane), kc = rs_kcol<T, true>(lane);
   f32x4 bav[2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) bav[mt] = a.ba ? bias4(a.ba, mt * 16 + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int mt = 0; mt < 2; ++mt) bav[mt] = a.ba ? bias4(a.ba, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
 
   // weight-gradient accumulators: wave w owns input-channel tile ct = w >> 1, output-channel tile ot = w & 1
   const int ct = wave >> 1, ot = wave & 1;
@@ -354,58 +432,62 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     bx.load(rs_rsrc((const T*)a.x + o, ibytes), tstart(tile) - 2 * d);
     by.load(rs_rsrc((const T*)a.dy + o, ibytes), tstart(tile) - d - 1);
   };
+  // A fragments from a weight image: lane reads row k*32 + mt*16 + pi(m), K slice kc
+  auto img_frag = [&](const T* img) {
+    const T* p = img + pn * WS + kc;
+    return [=](int k, int mt, int sc) { return M::load(p + (k * RC + mt * 16) * WS + sc * M::KS); };
+  };
   Rows32Buf<T, rs_pv<T>()> nx, ny;
   nx.init(XR);
   ny.init(YR);
   load_tile(nx, ny, tbeg);
-  nx.store(X);
-  ny.store(Y);
+  nx.template store<true>(X);
+  ny.template store<false>(Y);
   if (tbeg + 1 < tend) load_tile(nx, ny, tbeg + 1);
   __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
     const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
     // 1. recompute relu(h) over the dh rows (zero outside the item)
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
-    const int ko = M::koff(lane);
-    auto img_frag = [&](const T* img) {
-      return [=](int k, int mt, int sc) { return M::load(img + (k * RC + mt * 16 + (lane & 15)) * WS + ko + sc * M::KS); };
-    };
     int rh[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) rh[j] = min(wave + 4 * j, nht - 1) * 16;
     if (!(a.skip & 1)) {
       f32x4 acc[3][2];
-      conv_multi<T, true, 3>(acc, img_frag(waF), X, rh, d);
+      conv_multi<T, false, true, true, 3>(acc, img_frag(waF), X, rh, d);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= nht) continue;
-        const int i = rh[j] + (lane & 15), r = t0 - d + i;
-        const bool live = r >= 0 && r < a.T;
+        const int i = rh[j] + pn, r = t0 - d + i;
+        const bool live = interior || (r >= 0 && r < a.T);
+        f32x4 v[2];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          f32x4 v = acc[j][mt] + bav[mt];
+          v[mt] = acc[j][mt] + bav[mt];
           if (interior) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+            for (int q = 0; q < 4; ++q) v[mt][q] = fmaxf(v[mt][q], 0.f);
           } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = live ? fmaxf(v[q], 0.f) : 0.f;
+            for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
-          st4(H + i * XS + mt * 16 + 4 * (lane >> 4), v);
         }
+        st8(H + i * XS + oc, v[0], v[1]);
       }
     }
     __syncthreads();
     // 2a. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o], db_b += sum_t dy[t] (the tile's own rows)
-#pragma unroll 4
-    for (int kk = 0; kk < (a.skip & 2 ? 0 : RTM); kk += M::KS) {
-      const typename M::frag bf = M::rows(Y + (d + 1 + kk) * XS + ot * 16, XS);
+    if (!(a.skip & 2)) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const typename M::frag af = M::rows(H + (d + k - 1 + kk) * XS + ct * 16, XS);
-        gwb[k] = M::mma(af, bf, gwb[k]);
+      for (int kk = 0; kk < RTM; kk += M::KS) {
+        const typename M::frag bf = rs_rows(Y + (d + 1 + kk) * XS + ot * 16, XS);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const typename M::frag af = rs_rows(H + (d + k - 1 + kk) * XS + ct * 16, XS);
+          gwb[k] = M::mma(af, bf, gwb[k]);
+        }
+        if (ct == 0) gbb = M::mma(M::ones(), bf, gbb);
       }
-      if (ct == 0) gbb = M::mma(M::ones(), bf, gbb);
     }
     // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
     f32x4 dh[3][2];
@@ -413,15 +495,15 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       int rb[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = rh[j] + 2;
-      conv_multi<T, false, 3>(dh, img_frag(wbT), Y, rb, -1);
+      conv_multi<T, false, true, true, 3>(dh, img_frag(wbT), Y, rb, -1);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const int i = rh[j] + (lane & 15);
+        bool hp[8];
+        pos8(H + (rh[j] + pn) * XS + oc, hp);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const f32x4 hm = ld4(H + i * XS + mt * 16 + 4 * (lane >> 4));
-#pragma unroll
-          for (int q = 0; q < 4; ++q) dh[j][mt][q] = hm[q] > 0.f ? dh[j][mt][q] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          dh[j][0][q] = hp[q] ? dh[j][0][q] : 0.f;
+          dh[j][1][q] = hp[4 + q] ? dh[j][1][q] : 0.f;
         }
       }
     }
@@ -430,52 +512,50 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= nht) continue;
-        const int i = rh[j] + (lane & 15);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) st4(H + i * XS + mt * 16 + 4 * (lane >> 4), dh[j][mt]);
+        st8(H + (rh[j] + pn) * XS + oc, dh[j][0], dh[j][1]);
       }
     }
     __syncthreads();
     // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows
-    T* dxi = (T*)a.y + (size_t)n * a.T * RC;
     if (!(a.skip & 8)) {
+      const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + item_off(tile), ibytes);
       int rb[2];
       f32x4 acc[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16 + 2 * d;
-      conv_multi<T, false, 2>(acc, img_frag(waT), H, rb, -d);
+      conv_multi<T, false, true, true, 2>(acc, img_frag(waT), H, rb, -d);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int tl = (wave + 4 * j) * 16 + (lane & 15), t = t0 + tl;
-        if (t < a.T) {
+        const int tl = (wave + 4 * j) * 16 + pn;
+        bool xp[8];
+        f32x4 y0, y1;
+        pos8(X + (tl + 2 * d) * XS + oc, xp);
+        ld8(Y + (tl + d + 1) * XS + oc, y0, y1);
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) {
-            const int o = mt * 16 + 4 * (lane >> 4);
-            const f32x4 xm = ld4(X + (tl + 2 * d) * XS + o);
-            f32x4 v = acc[j][mt];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = xm[q] > 0.f ? v[q] : 0.f;
-            v = ld4(Y + (tl + d + 1) * XS + o) + v;
-            st4(dxi + (size_t)t * RC + o, v);
-          }
+        for (int q = 0; q < 4; ++q) {
+          y0[q] += xp[q] ? acc[j][0][q] : 0.f;
+          y1[q] += xp[4 + q] ? acc[j][1][q] : 0.f;
         }
+        st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
       }
     }
     // 4. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o], db_a += sum_t dh[t]
-#pragma unroll 4
-    for (int kk = 0; kk < (a.skip & 16 ? 0 : RTM); kk += M::KS) {
-      const typename M::frag bf = M::rows(H + (d + kk) * XS + ot * 16, XS);
+    if (!(a.skip & 16)) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const typename M::frag af = relu_frag(M::rows(X + ((k + 1) * d + kk) * XS + ct * 16, XS));
-        gwa[k] = M::mma(af, bf, gwa[k]);
+      for (int kk = 0; kk < RTM; kk += M::KS) {
+        const typename M::frag bf = rs_rows(H + (d + kk) * XS + ot * 16, XS);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const typename M::frag af = rs_rows(X + ((k + 1) * d + kk) * XS + ct * 16, XS);
+          gwa[k] = M::mma(af, bf, gwa[k]);
+        }
+        if (ct == 0) gba = M::mma(M::ones(), bf, gba);
       }
-      if (ct == 0) gba = M::mma(M::ones(), bf, gba);
     }
     if (tile + 1 < tend) {
       __syncthreads();  // every read of X, Y and H for this tile is done
-      nx.store(X);
-      ny.store(Y);
+      nx.template store<true>(X);
+      ny.template store<false>(Y);
       if (tile + 2 < tend) load_tile(nx, ny, tile + 2);
       __syncthreads();
     }
@@ -520,11 +600,12 @@ static size_t bwd_lds(int d, int esz) {
 }
 
 static int set_lds(const void* fn, size_t bytes) {
-  static size_t done[4] = {0, 0, 0, 0};
-  static const void* fns[4] = {nullptr, nullptr, nullptr, nullptr};
+  constexpr int NS = 32;
+  static size_t done[NS] = {};
+  static const void* fns[NS] = {};
   if (bytes <= 65536) return VQA_OK;
   int slot = 0;
-  while (slot < 3 && fns[slot] && fns[slot] != fn) ++slot;
+  while (slot < NS - 1 && fns[slot] && fns[slot] != fn) ++slot;
   if (fns[slot] == fn && done[slot] >= bytes) return VQA_OK;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
     (void)hipGetLastError();
@@ -534,6 +615,23 @@ static int set_lds(const void* fn, size_t bytes) {
   fns[slot] = fn;
   done[slot] = bytes;
   return VQA_OK;
+}
+
+// kernel instance for a dilation: the model's dilations (3^i, i < 4) are compiled constants
+template <class T> struct RsFwd {
+  template <int D> static const void* fn() { return (const void*)resblock_fwd_kernel<T, D>; }
+};
+template <class T> struct RsBwd {
+  template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D>; }
+};
+template <class F> static const void* rs_pick(int d) {
+  switch (d) {
+    case 1: return F::template fn<1>();
+    case 3: return F::template fn<3>();
+    case 9: return F::template fn<9>();
+    case 27: return F::template fn<27>();
+    default: return F::template fn<0>();
+  }
 }
 
 static void plan(ResArgs& a, int per_cu) {
@@ -567,13 +665,10 @@ extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba,
   const size_t lds = fwd_lds(RMAXD, esz);  // one LDS reservation for every dilation
   const hipStream_t s = (hipStream_t)stream;
   const dim3 grid((a.ntiles + a.tpw - 1) / a.tpw);
-  if (dtype == VQA_BF16) {
-    if (int rc = set_lds((const void*)resblock_fwd_kernel<bf16>, lds)) return rc;
-    hipLaunchKernelGGL(resblock_fwd_kernel<bf16>, grid, dim3(256), lds, s, a);
-  } else {
-    if (int rc = set_lds((const void*)resblock_fwd_kernel<float>, lds)) return rc;
-    hipLaunchKernelGGL(resblock_fwd_kernel<float>, grid, dim3(256), lds, s, a);
-  }
+  const void* fn = dtype == VQA_BF16 ? rs_pick<RsFwd<bf16>>(dilation) : rs_pick<RsFwd<float>>(dilation);
+  if (int rc = set_lds(fn, lds)) return rc;
+  void* args[] = {&a};
+  (void)hipLaunchKernel(fn, grid, dim3(256), args, lds, s);
   VQA_LAUNCHED("resblock_fwd_kernel");
   return VQA_OK;
 }
@@ -611,13 +706,10 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   const size_t lds = bwd_lds(dilation, esz);
   const size_t lds_max = bwd_lds(RMAXD, esz);
   const hipStream_t s = (hipStream_t)stream;
-  if (dtype == VQA_BF16) {
-    if (int rc = set_lds((const void*)resblock_bwd_kernel<bf16>, lds_max)) return rc;
-    hipLaunchKernelGGL(resblock_bwd_kernel<bf16>, dim3(nwg), dim3(256), lds, s, a);
-  } else {
-    if (int rc = set_lds((const void*)resblock_bwd_kernel<float>, lds_max)) return rc;
-    hipLaunchKernelGGL(resblock_bwd_kernel<float>, dim3(nwg), dim3(256), lds, s, a);
-  }
+  const void* fn = dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation);
+  if (int rc = set_lds(fn, lds_max)) return rc;
+  void* args[] = {&a};
+  (void)hipLaunchKernel(fn, dim3(nwg), dim3(256), args, lds, s);
   VQA_LAUNCHED("resblock_bwd_kernel");
   const vqa_partials_desc da{a.part_a, dwa, dba, nwg, E, 3 * RC * RC, 0};
   const vqa_partials_desc dbd{a.part_b, dwb, dbb, nwg, E, 3 * RC * RC, 0};
