@@ -818,8 +818,7 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
   const int tbeg = ch * a.CH, tend = min(a.T_out, tbeg + a.CH);
   const int rows_in = (TT - 1) * a.S + (a.K - 1) * a.D + 1;
   const int ntile = a.K * CT * OT;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ko = (int)sizeof(T) == 2 ? 8 * (lane >> 4) : (lane >> 4);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 
   f32x4 acc[MAXTW];
 #pragma unroll
@@ -863,12 +862,14 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
       const int tile = wave + 4 * ti;
       if (tile < ntile) {
         const int ot = tile % OT, rest = tile / OT, ct = rest % CT, k = rest / CT;
-        const T* xp = xl + (size_t)(k * a.D + ko * a.S) * XS + ct * 16 + (lane & 15);
-        const T* gp = gl + (size_t)ko * GS + ot * 16 + (lane & 15);
+        // K = output rows: transposed LDS reads of both operands (same even/odd K order)
+        const T* xp = xl + (size_t)(k * a.D) * XS + ct * 16;
+        const T* gp = gl + ot * 16;
         f32x4 c = acc[ti];
+#pragma unroll
         for (int kk = 0; kk < TT; kk += KT) {
-          const typename M::frag af = M::gather(xp + (size_t)(kk * a.S) * XS, a.S * XS);
-          const typename M::frag bf = M::gather(gp + (size_t)kk * GS, GS);
+          const typename M::frag af = M::rows_eo(xp + (size_t)(kk * a.S) * XS, a.S * XS);
+          const typename M::frag bf = M::rows_eo(gp + (size_t)kk * GS, GS);
           c = M::mma(af, bf, c);
         }
         acc[ti] = c;

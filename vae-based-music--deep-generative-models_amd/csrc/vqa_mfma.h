@@ -40,6 +40,18 @@ template <> struct Mfma<bf16> {
     typedef short v8s __attribute__((ext_vector_type(8)));
     return __builtin_bit_cast(frag, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   }
+  // the same 32 rows under another K order: lanes 0-31 take the even rows, lanes 32-63 the odd rows. Both
+  // operands of a product must use the same order. With a row stride of 20 or 36 dwords (32 or 64 bf16
+  // channels + 16 B of padding) each read is free of bank conflicts (rows() is 2-way there).
+  static __device__ __forceinline__ frag rows_eo(const bf16* o, int stride) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const bf16* a0 = o + (2 * (4 * (g & 1) + (i >> 2)) + (g >> 1)) * stride + 4 * (i & 3);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 16 * stride));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    return __builtin_bit_cast(frag, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
 };
 template <> struct Mfma<float> {
   static constexpr int KS = 4;
@@ -55,6 +67,7 @@ template <> struct Mfma<float> {
     const int l = threadIdx.x & 63;
     return o[(l >> 4) * stride + (l & 15)];
   }
+  static __device__ __forceinline__ frag rows_eo(const float* o, int stride) { return rows(o, stride); }
 };
 
 template <class T> __device__ __forceinline__ void relu_bits(uint4& v);
