@@ -139,6 +139,20 @@ int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, const float
                      int dtype, void* workspace, size_t ws_bytes, vqa_partials_desc* desc, vqa_stream_t stream);
 size_t vqa_resblock_bwd_workspace(int B, int T, int C, int dilation, int dtype);
 
+/* ---- decoder tail: the last Conv1DTranspose (K=4, stride 2, C -> Cu) of the last decoder block followed by
+ *      the decoder's output Conv1D (K=3, Cu -> 1), encdec.py:67-68 then :148, with nothing in between, run as
+ *      ONE thin 3-tap convolution from h (B, T, C) to y (B, 2T, 1) fp32 (the two linear maps composed; the
+ *      Cu-channel full-rate tensor is never formed). Backward: dh (B, T, C) and the four parameter gradients
+ *      (written, not accumulated) from dy (B, 2T, 1) fp32. C must be 32. */
+int vqa_dtail_supported(int C, int Cu, int K_up, int stride_up, int K_out, int C_out, int dtype);
+size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype);
+int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up, const float* w_out, const float* b_out,
+                  float* y, int B, int T, int C, int Cu, int dtype, void* workspace, size_t ws_bytes,
+                  vqa_stream_t stream);
+int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, const float* b_up, const float* w_out,
+                  const float* b_out, void* dh, float* dw_up, float* db_up, float* dw_out, float* db_out, int B,
+                  int T, int C, int Cu, int dtype, void* workspace, size_t ws_bytes, vqa_stream_t stream);
+
 /* ---- Vector quantizer (VectorQuantizer.py) ---------------------------------------------------- */
 /* e_sqnorm[k] = sum_d E[d][k]^2  (VectorQuantizer.py:180). E is (D, K). */
 int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream);

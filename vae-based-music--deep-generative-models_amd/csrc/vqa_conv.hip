@@ -1116,29 +1116,34 @@ __global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
   if (threadIdx.x < a.nb) out[E + threadIdx.x] = dbacc;
 }
 
-// out1[e] = sum_p ws[p*E + e] for e < E1, out2[e - E1] likewise for e >= E1. Block = 64 elements x 4
-// part groups; each thread keeps 4 independent partial sums (memory-level parallelism); the groups are
-// combined in a fixed order, so the result is deterministic.
-__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, int nparts, int E, int E1,
-                                                             float* out1, float* out2) {
-  __shared__ float red[4][64];
-  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + el;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+// out1[e] = sum_p ws[p*E + e] for e < E1, out2[e - E1] likewise for e >= E1. Block = 16 elements x 16 part
+// groups (64-byte row segments); each thread keeps 8 independent partial sums (memory-level parallelism);
+// the sums and then the groups are combined in a fixed order, so the result is deterministic.
+constexpr int kRedCols = 16;
+__device__ __forceinline__ float reduce_col16(const float* ws, int nparts, int E, int e, float (*red)[kRedCols]) {
+  const int el = threadIdx.x & (kRedCols - 1), grp = threadIdx.x / kRedCols;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (e < E) {
     int p = grp;
-    for (; p + 12 < nparts; p += 16) {
-      s0 += ws[(size_t)p * E + e];
-      s1 += ws[(size_t)(p + 4) * E + e];
-      s2 += ws[(size_t)(p + 8) * E + e];
-      s3 += ws[(size_t)(p + 12) * E + e];
-    }
-    for (; p < nparts; p += 4) s0 += ws[(size_t)p * E + e];
+    for (; p + 7 * 16 < nparts; p += 8 * 16)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += ws[(size_t)(p + 16 * u) * E + e];
+    for (; p < nparts; p += 16) s[0] += ws[(size_t)p * E + e];
   }
-  red[grp][el] = (s0 + s1) + (s2 + s3);
+  red[grp][el] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
-  if (grp == 0 && e < E) {
-    const float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+  float t = 0.f;
+  if (grp == 0)
+    for (int g = 0; g < 16; ++g) t += red[g][el];
+  return t;
+}
+
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, int nparts, int E, int E1,
+                                                             float* out1, float* out2) {
+  __shared__ float red[16][kRedCols];
+  const int e = blockIdx.x * kRedCols + (threadIdx.x & (kRedCols - 1));
+  const float s = reduce_col16(ws, nparts, E, e, red);
+  if (threadIdx.x < kRedCols && e < E) {
     if (e < E1) {
       if (out1) out1[e] = s;
     } else if (out2) {
@@ -1148,7 +1153,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, i
 }
 
 // Batched form: one launch reduces up to kMaxDescs layers; block b belongs to the descriptor whose
-// [start, start + ceil(n/64)) range contains it. Same fixed summation order as reduce_partials_kernel.
+// [start, start + ceil(n/16)) range contains it. Same fixed summation order as reduce_partials_kernel.
 constexpr int kMaxDescs = 48;
 struct ReduceBatch {
   vqa_partials_desc d[kMaxDescs];
@@ -1157,29 +1162,13 @@ struct ReduceBatch {
 };
 
 __global__ __launch_bounds__(256) void reduce_partials_batched_kernel(ReduceBatch rb) {
-  __shared__ float red[4][64];
+  __shared__ float red[16][kRedCols];
   int i = 0;
   while (i + 1 < rb.count && (int)blockIdx.x >= rb.start[i + 1]) ++i;
   const vqa_partials_desc& d = rb.d[i];
-  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int e = ((int)blockIdx.x - rb.start[i]) * 64 + el;
-  const int E = d.n, nparts = d.nparts;
-  const float* ws = d.partials;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (e < E) {
-    int p = grp;
-    for (; p + 12 < nparts; p += 16) {
-      s0 += ws[(size_t)p * E + e];
-      s1 += ws[(size_t)(p + 4) * E + e];
-      s2 += ws[(size_t)(p + 8) * E + e];
-      s3 += ws[(size_t)(p + 12) * E + e];
-    }
-    for (; p < nparts; p += 4) s0 += ws[(size_t)p * E + e];
-  }
-  red[grp][el] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (grp == 0 && e < E) {
-    const float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+  const int e = ((int)blockIdx.x - rb.start[i]) * kRedCols + (threadIdx.x & (kRedCols - 1));
+  const float s = reduce_col16(d.partials, d.nparts, d.n, e, red);
+  if (threadIdx.x < kRedCols && e < d.n) {
     if (e < d.n_w) {
       if (d.dw) d.dw[e] = s;
     } else if (d.db) {
@@ -1601,7 +1590,7 @@ int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_i
     *defer = vqa_partials_desc{(const float*)ws, dw, db, p.nwg, p.E, KCO, 0};
     return VQA_OK;
   }
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((p.E + 63) / 64), dim3(256), 0, s, (const float*)ws, p.nwg, p.E,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((p.E + kRedCols - 1) / kRedCols), dim3(256), 0, s, (const float*)ws, p.nwg, p.E,
                      KCO, dw, db);
   VQA_LAUNCHED("reduce_partials_kernel");
   return VQA_OK;
@@ -1809,7 +1798,7 @@ extern "C" int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const 
       *desc = vqa_partials_desc{(const float*)workspace, dw, db, nparts, E, KCO, 0};
       return VQA_OK;
     }
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((E + 63) / 64), dim3(256), 0, s, (const float*)workspace, nparts, E,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((E + kRedCols - 1) / kRedCols), dim3(256), 0, s, (const float*)workspace, nparts, E,
                        KCO, dw, db);
     VQA_LAUNCHED("reduce_partials_kernel");
     return VQA_OK;
@@ -1829,7 +1818,7 @@ extern "C" int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const 
         *desc = vqa_partials_desc{(const float*)workspace, dw, db, nwg, E, KCO, 0};
         return VQA_OK;
       }
-      hipLaunchKernelGGL(reduce_partials_kernel, dim3((E + 63) / 64), dim3(256), 0, s, (const float*)workspace, nwg, E,
+      hipLaunchKernelGGL(reduce_partials_kernel, dim3((E + kRedCols - 1) / kRedCols), dim3(256), 0, s, (const float*)workspace, nwg, E,
                          KCO, dw, db);
       VQA_LAUNCHED("reduce_partials_kernel");
       return VQA_OK;
@@ -1857,7 +1846,7 @@ extern "C" int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vq
       VQA_ARG(d.partials && d.n > 0 && d.nparts > 0 && d.n_w <= d.n, "reduce_partials: bad descriptor %d", base + i);
       rb.d[i] = d;
       rb.start[i] = blocks;
-      blocks += (d.n + 63) / 64;
+      blocks += (d.n + kRedCols - 1) / kRedCols;
     }
     rb.start[rb.count] = blocks;
     hipLaunchKernelGGL(reduce_partials_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);

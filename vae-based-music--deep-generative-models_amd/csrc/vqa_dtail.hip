@@ -1,0 +1,460 @@
+// vqa_dtail.hip — the decoder tail: the last Conv1DTranspose of the last decoder block followed by the
+// decoder's output Conv1D (encdec.py:67-68 then :148), as ONE thin convolution (gfx950).
+//
+// Nothing sits between the two layers, so the composition is linear in h (the transposed conv's input,
+// C = 32 channels at T rows per item):
+//     u[s]  = b_up + sum_{kb, j: s = 2j + kb - 1} W_up[kb] h[j]            (K=4, stride 2, SAME: pad 1)
+//     y[t]  = b_out + sum_k W_out[k] . u[t + k - 1]                        (K=3, SAME, u[-1] = u[2T] = 0)
+//  => y[2j + p] = bias + sum_{a=-1..1} sum_c V[a][c][p] h[j + a][c]        (p = 0, 1: the two output phases)
+// with V[a][c][p] = sum_k sum_o W_out[k][o] W_up[p + k - 2a][o][c] (terms with p + k - 2a outside 0..3
+// vanish) and two edge corrections per item (the out conv's zero padding at t = 0 and t = 2T - 1 drops
+// tap k = 0 resp. k = 2). The 64-channel full-rate tensor u is never formed: the forward reads h and
+// writes y, the backward reads h and dy and writes dh, and the parameter gradients follow from
+// dV = sum h (x) dy by the chain rule through the (bilinear) composition. Same function as the reference's
+// two layers; only the association of the sums differs (u is not rounded to the activation dtype).
+//
+// Lanes: 4 lanes per row, each owning 8 consecutive channels (one 16-byte bf16 chunk), 16 rows per wave
+// instruction; the 3-tap window re-reads neighbour rows through the caches.
+#include "vqa_common.h"
+
+namespace vqa {
+
+constexpr int DT_C = 32;   // transposed-conv input channels the lane map covers
+constexpr int DT_NV = 192; // V[3][32][2]
+// composite workspace: V | edge0[32] | edge1[32] | bias_int, b0, b2, (pad)
+constexpr int DT_COMP = DT_NV + 2 * DT_C + 4;
+// backward partial row: dV[3][32][2] | Eh[32] | Et[32] | S, F, L, (pad)
+constexpr int DT_PART = DT_NV + 2 * DT_C + 4;
+
+// 8 channels held packed until use (bf16: one 16-byte load), so several rows' loads can be in flight
+template <class T> struct Raw8;
+template <> struct Raw8<bf16> {
+  uint4 w;
+  __device__ __forceinline__ void load(const bf16* p, bool ok) { w = ok ? *(const uint4*)p : uint4{0u, 0u, 0u, 0u}; }
+  __device__ __forceinline__ void get(float (&v)[8]) const {
+    const unsigned u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p, bool ok) {
+    a = b = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ok) {
+      a = *(const f32x4*)p;
+      b = *(const f32x4*)(p + 4);
+    }
+  }
+  __device__ __forceinline__ void get(float (&v)[8]) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[i + 4] = b[i];
+    }
+  }
+};
+
+template <class T> __device__ __forceinline__ void dt_store8(T* p, const float (&v)[8]);
+template <> __device__ __forceinline__ void dt_store8<bf16>(bf16* p, const float (&v)[8]) {
+  bf16x8 x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = (bf16)v[i];
+  *(bf16x8*)p = x;
+}
+template <> __device__ __forceinline__ void dt_store8<float>(float* p, const float (&v)[8]) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+// V, edge vectors and bias terms from the two layers' weights: one wave per output (the sum over the Cu
+// channels split across the lanes, then a fixed-order wave reduction); DT_COMP_WAVES waves in all
+constexpr int DT_COMP_WAVES = DT_NV + 2 * DT_C + 1;
+__global__ __launch_bounds__(256) void dtail_compose_kernel(const float* w_up, const float* b_up, const float* w_out,
+                                                            const float* b_out, int Cu, float* comp) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (e >= DT_COMP_WAVES) return;
+  if (e < DT_NV + 2 * DT_C) {
+    float s = 0.f;
+    if (e < DT_NV) {
+      const int a = e / (2 * DT_C) - 1, c = (e >> 1) % DT_C, p = e & 1;
+      for (int k = 0; k < 3; ++k) {
+        const int kb = p + k - 2 * a;
+        if (kb < 0 || kb > 3) continue;
+        for (int o = lane; o < Cu; o += 64) s += w_out[k * Cu + o] * w_up[((size_t)kb * Cu + o) * DT_C + c];
+      }
+    } else {
+      const int c = (e - DT_NV) % DT_C, edge = (e - DT_NV) / DT_C;  // edge 0: (k=0, kb=0); 1: (k=2, kb=3)
+      const int k = edge ? 2 : 0, kb = edge ? 3 : 0;
+      for (int o = lane; o < Cu; o += 64) s += w_out[k * Cu + o] * w_up[((size_t)kb * Cu + o) * DT_C + c];
+    }
+    s = warp_sum(s);
+    if (lane == 0) comp[e] = s;
+  } else {
+    float bk[3] = {0.f, 0.f, 0.f};
+    for (int o = lane; o < Cu; o += 64) {
+      const float bu = b_up ? b_up[o] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) bk[k] += w_out[k * Cu + o] * bu;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bk[k] = warp_sum(bk[k]);
+    if (lane == 0) {
+      const float bo = b_out ? b_out[0] : 0.f;
+      comp[DT_NV + 2 * DT_C] = bo + bk[0] + bk[1] + bk[2];
+      comp[DT_NV + 2 * DT_C + 1] = bk[0];
+      comp[DT_NV + 2 * DT_C + 2] = bk[2];
+      comp[DT_NV + 2 * DT_C + 3] = 0.f;
+    }
+  }
+}
+
+struct DtArgs {
+  const void* h;    // (B, T, 32)
+  const float* dy;  // backward: (B, 2T) fp32
+  float* y;         // forward: (B, 2T) fp32
+  void* dh;         // backward: (B, T, 32)
+  const float* comp;
+  float* part;      // backward: [gridDim.x][DT_PART]
+  int B, T;
+};
+
+// y[n, 2j + p] for 16 rows per wave and iteration (grid-stride over the B*T rows)
+template <class T>
+__global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
+  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3;
+  float v[3][8][2], e0[8], e1[8];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) v[t][i][p] = a.comp[(t * DT_C + 8 * q + i) * 2 + p];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    e0[i] = a.comp[DT_NV + 8 * q + i];
+    e1[i] = a.comp[DT_NV + DT_C + 8 * q + i];
+  }
+  const float bias = a.comp[DT_NV + 2 * DT_C], b0 = a.comp[DT_NV + 2 * DT_C + 1], b2 = a.comp[DT_NV + 2 * DT_C + 2];
+  const T* H = (const T*)a.h;
+  const long long rows = (long long)a.B * a.T;
+  constexpr int U = 4;  // row groups of 16 per wave and iteration, all loads issued first
+  const long long step = (long long)gridDim.x * 64 * U;
+  for (long long R0 = (long long)blockIdx.x * 64 * U + (threadIdx.x >> 6) * 16 * U; R0 < rows; R0 += step) {
+    Raw8<T> raw[U][3];
+    int nn[U], jj[U];
+    bool lv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long R = R0 + 16 * u + r;
+      lv[u] = R < rows;
+      nn[u] = lv[u] ? (int)(R / a.T) : 0;
+      jj[u] = lv[u] ? (int)(R - (long long)nn[u] * a.T) : 0;
+      const T* hr = H + ((long long)nn[u] * a.T + jj[u]) * DT_C + 8 * q;
+      raw[u][0].load(hr - DT_C, lv[u] && jj[u] > 0);
+      raw[u][1].load(hr, lv[u]);
+      raw[u][2].load(hr + DT_C, lv[u] && jj[u] + 1 < a.T);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = nn[u], j = jj[u];
+      float hm[8], h0[8], hp[8];
+      raw[u][0].get(hm);
+      raw[u][1].get(h0);
+      raw[u][2].get(hp);
+      float y0 = 0.f, y1 = 0.f, c0 = 0.f, c1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        y0 += v[0][i][0] * hm[i] + v[1][i][0] * h0[i] + v[2][i][0] * hp[i];
+        y1 += v[0][i][1] * hm[i] + v[1][i][1] * h0[i] + v[2][i][1] * hp[i];
+        c0 += e0[i] * h0[i];
+        c1 += e1[i] * h0[i];
+      }
+      if (j == 0) y0 -= c0;        // out conv padding at t = 0 drops tap k = 0
+      if (j == a.T - 1) y1 -= c1;  // ... and at t = 2T - 1 tap k = 2
+      y0 += __shfl_xor(y0, 1, 64);
+      y1 += __shfl_xor(y1, 1, 64);
+      y0 += __shfl_xor(y0, 2, 64);
+      y1 += __shfl_xor(y1, 2, 64);
+      if (lv[u] && q == 0) {
+        y0 += bias - (j == 0 ? b0 : 0.f);
+        y1 += bias - (j == a.T - 1 ? b2 : 0.f);
+        *(float2*)(a.y + ((long long)n * a.T + j) * 2) = make_float2(y0, y1);
+      }
+    }
+  }
+}
+
+// dh (adjoint of the composite) and the per-workgroup partial row of dV / edge sums / dy sums
+template <class T>
+__global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
+  __shared__ float red[4][4][68];  // [wave][q][element of the lane's slice]
+  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3, wave = threadIdx.x >> 6;
+  float v[3][8][2], e0[8], e1[8];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) v[t][i][p] = a.comp[(t * DT_C + 8 * q + i) * 2 + p];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    e0[i] = a.comp[DT_NV + 8 * q + i];
+    e1[i] = a.comp[DT_NV + DT_C + 8 * q + i];
+  }
+  float dv[3][8][2], eh[8], et[8], sS = 0.f, sF = 0.f, sL = 0.f;
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dv[t][i][0] = dv[t][i][1] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eh[i] = et[i] = 0.f;
+  const T* H = (const T*)a.h;
+  T* DH = (T*)a.dh;
+  const long long rows = (long long)a.B * a.T;
+  const long long step = (long long)gridDim.x * (blockDim.x >> 2);
+  const int T2 = 2 * a.T;
+  constexpr int U = 2;
+  for (long long R0 = (long long)blockIdx.x * 64 * U + wave * 16 * U; R0 < rows; R0 += step * U) {
+    Raw8<T> raw[U];
+    float g[U][6];  // dy[2j - 2 .. 2j + 3] (zero outside the item)
+    int nn[U], jj[U];
+    bool lv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long R = R0 + 16 * u + r;
+      lv[u] = R < rows;
+      nn[u] = lv[u] ? (int)(R / a.T) : 0;
+      jj[u] = lv[u] ? (int)(R - (long long)nn[u] * a.T) : 0;
+      const float* dyn = a.dy + (long long)nn[u] * T2;
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int t = 2 * jj[u] - 2 + 2 * m;
+        float2 w = make_float2(0.f, 0.f);
+        if (lv[u] && t >= 0 && t < T2) w = *(const float2*)(dyn + t);
+        g[u][2 * m] = w.x;
+        g[u][2 * m + 1] = w.y;
+      }
+      raw[u].load(H + ((long long)nn[u] * a.T + jj[u]) * DT_C + 8 * q, lv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = nn[u], j = jj[u];
+      const float* gg = g[u];
+      float h0[8];
+      raw[u].get(h0);
+      // dh[j][c] = sum_{a,p} V[a][c][p] dy[2(j - a) + p]: a = -1 -> gg[4 + p], a = 0 -> gg[2 + p], a = 1 -> gg[p]
+      float d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        d[i] = v[0][i][0] * gg[4] + v[0][i][1] * gg[5] + v[1][i][0] * gg[2] + v[1][i][1] * gg[3] +
+               v[2][i][0] * gg[0] + v[2][i][1] * gg[1];
+        if (j == 0) d[i] -= e0[i] * gg[2];
+        if (j == a.T - 1) d[i] -= e1[i] * gg[3];
+      }
+      if (lv[u]) dt_store8<T>(DH + ((long long)n * a.T + j) * DT_C + 8 * q, d);
+      // dV[a][c][p] = sum_j h[j + a][c] dy[2j + p] = sum_j h[j][c] dy[2(j - a) + p]: row j's own h against the
+      // same dy window (out-of-item dy reads are zero); edge sums; dy sums (q == 0 lanes only)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dv[0][i][0] += h0[i] * gg[4];
+        dv[0][i][1] += h0[i] * gg[5];
+        dv[1][i][0] += h0[i] * gg[2];
+        dv[1][i][1] += h0[i] * gg[3];
+        dv[2][i][0] += h0[i] * gg[0];
+        dv[2][i][1] += h0[i] * gg[1];
+        if (j == 0) eh[i] += h0[i] * gg[2];
+        if (j == a.T - 1) et[i] += h0[i] * gg[3];
+      }
+      if (q == 0 && lv[u]) {
+        sS += gg[2] + gg[3];
+        if (j == 0) sF += gg[2];
+        if (j == a.T - 1) sL += gg[3];
+      }
+    }
+  }
+  // per-lane slice (64 values: dv 48 | eh 8 | et 8; q == 0 adds S, F, L) -> sum over the 16 rows of the
+  // wave (lanes with equal q), then over the 4 waves, in a fixed order
+  float s[67];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s[(t * 8 + i) * 2] = dv[t][i][0];
+      s[(t * 8 + i) * 2 + 1] = dv[t][i][1];
+    }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s[48 + i] = eh[i];
+    s[56 + i] = et[i];
+  }
+  s[64] = sS;
+  s[65] = sF;
+  s[66] = sL;
+#pragma unroll
+  for (int e = 0; e < 67; ++e) {
+    float x = s[e];
+    x += __shfl_xor(x, 4, 64);
+    x += __shfl_xor(x, 8, 64);
+    x += __shfl_xor(x, 16, 64);
+    x += __shfl_xor(x, 32, 64);
+    s[e] = x;
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int e = 0; e < 67; ++e) red[wave][q][e] = s[e];
+  }
+  __syncthreads();
+  float* out = a.part + (size_t)blockIdx.x * DT_PART;
+  for (int e = threadIdx.x; e < DT_PART; e += 256) {
+    // element e of the partial row -> (q, slice index)
+    int qq, si;
+    if (e < DT_NV) {
+      const int t = e / (2 * DT_C), c = (e >> 1) % DT_C, p = e & 1;
+      qq = c >> 3;
+      si = (t * 8 + (c & 7)) * 2 + p;
+    } else if (e < DT_NV + 2 * DT_C) {
+      const int c = (e - DT_NV) % DT_C, which = (e - DT_NV) / DT_C;
+      qq = c >> 3;
+      si = 48 + 8 * which + (c & 7);
+    } else {
+      qq = 0;
+      si = 64 + (e - DT_NV - 2 * DT_C);
+    }
+    float x = 0.f;
+    if (si < 67)
+      for (int w = 0; w < 4; ++w) x += red[w][qq][si];
+    out[e] = x;
+  }
+}
+
+// parameter gradients from the reduced partial row. Blocks [0, nbo): one wave per dW_out element (the
+// 192-term sum split across the lanes); blocks [nbo, ...): one thread per dW_up element, then db_up, db_out
+__global__ __launch_bounds__(256) void dtail_chain_kernel(const float* red, const float* w_up, const float* b_up,
+                                                          const float* w_out, int Cu, int nbo, float* dw_up,
+                                                          float* db_up, float* dw_out, float* db_out) {
+  const float* dV = red;
+  const float* Eh = red + DT_NV;
+  const float* Et = red + DT_NV + DT_C;
+  const float S = red[DT_NV + 2 * DT_C], F = red[DT_NV + 2 * DT_C + 1], L = red[DT_NV + 2 * DT_C + 2];
+  // gradient of the per-tap composite V_k: the shared dV plus the edge terms of taps 0 and 2
+  auto dvk = [&](int k, int a, int c, int p) {
+    float x = dV[((a + 1) * DT_C + c) * 2 + p];
+    if (k == 0 && a == 0 && p == 0) x -= Eh[c];
+    if (k == 2 && a == 0 && p == 1) x -= Et[c];
+    return x;
+  };
+  auto sk = [&](int k) { return S - (k == 0 ? F : 0.f) - (k == 2 ? L : 0.f); };
+  if ((int)blockIdx.x < nbo) {
+    // dW_out[k][o] = sum_{a, p, c} dV_k[a][c][p] W_up[p + k - 2a][o][c] + b_up[o] S_k
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (e >= 3 * Cu) return;
+    const int k = e / Cu, o = e % Cu;
+    float x = 0.f;
+    for (int t = lane; t < DT_NV; t += 64) {
+      const int a = t / (2 * DT_C) - 1, c = (t >> 1) % DT_C, p = t & 1, kb = p + k - 2 * a;
+      if (kb >= 0 && kb <= 3) x += dvk(k, a, c, p) * w_up[((size_t)kb * Cu + o) * DT_C + c];
+    }
+    x = warp_sum(x);
+    if (lane == 0) dw_out[e] = x + (b_up ? b_up[o] : 0.f) * sk(k);
+    return;
+  }
+  const int e = (blockIdx.x - nbo) * 256 + threadIdx.x;
+  if (e < 4 * Cu * DT_C) {
+    // dW_up[kb][o][c] = sum_{k, a, p: p + k - 2a = kb} dV_k[a][c][p] W_out[k][o]
+    const int kb = e / (Cu * DT_C), o = (e / DT_C) % Cu, c = e % DT_C;
+    float x = 0.f;
+    for (int k = 0; k < 3; ++k)
+      for (int p = 0; p < 2; ++p) {
+        const int t2 = p + k - kb;  // = 2a
+        if (t2 & 1) continue;
+        const int a = t2 / 2;
+        if (a < -1 || a > 1) continue;
+        x += dvk(k, a, c, p) * w_out[k * Cu + o];
+      }
+    dw_up[e] = x;
+  } else if (e < 4 * Cu * DT_C + Cu) {
+    const int o = e - 4 * Cu * DT_C;
+    float x = 0.f;
+    for (int k = 0; k < 3; ++k) x += w_out[k * Cu + o] * sk(k);
+    if (db_up) db_up[o] = x;
+  } else if (e == 4 * Cu * DT_C + Cu) {
+    if (db_out) db_out[0] = S;
+  }
+}
+
+static int dt_grid(long long rows) {
+  // 64 rows per workgroup and iteration; about 4 resident workgroups per CU
+  long long g = (rows + 63) / 64;
+  const long long cap = 1024;
+  return (int)(g < cap ? (g > 0 ? g : 1) : cap);
+}
+
+}  // namespace vqa
+
+using namespace vqa;
+
+extern "C" int vqa_dtail_supported(int C, int Cu, int K_up, int stride_up, int K_out, int C_out, int dtype) {
+  return C == DT_C && Cu >= 1 && Cu <= 1024 && K_up == 4 && stride_up == 2 && K_out == 3 && C_out == 1 &&
+         (dtype == VQA_BF16 || dtype == VQA_F32);
+}
+
+extern "C" size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype) {
+  (void)C;
+  (void)Cu;
+  (void)dtype;
+  const int g = dt_grid((long long)B * T);
+  return ((size_t)DT_COMP + (size_t)DT_PART + (size_t)g * DT_PART) * sizeof(float);
+}
+
+extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up, const float* w_out,
+                             const float* b_out, float* y, int B, int T, int C, int Cu, int dtype, void* workspace,
+                             size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(h && w_up && w_out && y && B > 0 && T > 0, "dtail_fwd: bad arguments");
+  VQA_REQUIRE(vqa_dtail_supported(C, Cu, 4, 2, 3, 1, dtype), VQA_E_UNSUPPORTED, "dtail_fwd: unsupported C=%d Cu=%d",
+              C, Cu);
+  VQA_ARG(workspace && ws_bytes >= vqa_dtail_workspace(B, T, C, Cu, dtype), "dtail_fwd: workspace too small");
+  const hipStream_t s = (hipStream_t)stream;
+  float* comp = (float*)workspace;
+  hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
+                     Cu, comp);
+  VQA_LAUNCHED("dtail_compose_kernel");
+  DtArgs a{h, nullptr, y, nullptr, comp, nullptr, B, T};
+  const int g = dt_grid((long long)B * T);
+  if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_fwd_kernel<bf16>, dim3(g), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dtail_fwd_kernel<float>, dim3(g), dim3(256), 0, s, a);
+  VQA_LAUNCHED("dtail_fwd_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, const float* b_up,
+                             const float* w_out, const float* b_out, void* dh, float* dw_up, float* db_up,
+                             float* dw_out, float* db_out, int B, int T, int C, int Cu, int dtype, void* workspace,
+                             size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(dy && h && w_up && w_out && dh && dw_up && dw_out && B > 0 && T > 0, "dtail_bwd: bad arguments");
+  VQA_REQUIRE(vqa_dtail_supported(C, Cu, 4, 2, 3, 1, dtype), VQA_E_UNSUPPORTED, "dtail_bwd: unsupported C=%d Cu=%d",
+              C, Cu);
+  VQA_ARG(workspace && ws_bytes >= vqa_dtail_workspace(B, T, C, Cu, dtype), "dtail_bwd: workspace too small");
+  const hipStream_t s = (hipStream_t)stream;
+  float* comp = (float*)workspace;
+  float* red = comp + DT_COMP;
+  float* part = red + DT_PART;
+  hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
+                     Cu, comp);
+  VQA_LAUNCHED("dtail_compose_kernel");
+  const int g = dt_grid((long long)B * T);
+  DtArgs a{h, dy, nullptr, dh, comp, part, B, T};
+  if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_bwd_kernel<bf16>, dim3(g), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dtail_bwd_kernel<float>, dim3(g), dim3(256), 0, s, a);
+  VQA_LAUNCHED("dtail_bwd_kernel");
+  const vqa_partials_desc d{part, red, nullptr, g, DT_PART, DT_PART, 0};
+  if (int rc = vqa_reduce_partials(&d, 1, stream)) return rc;
+  const int nbo = (3 * Cu + 3) / 4, nbu = (4 * Cu * DT_C + Cu + 1 + 255) / 256;
+  hipLaunchKernelGGL(dtail_chain_kernel, dim3(nbo + nbu), dim3(256), 0, s, red, w_up, b_up, w_out, Cu, nbo, dw_up,
+                     db_up, dw_out, db_out);
+  VQA_LAUNCHED("dtail_chain_kernel");
+  return VQA_OK;
+}

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import torch
 
+import vqa_lib as V
 from resnet import DilatedResnet1D
 from vqa_layers import Conv1D, Conv1DTranspose
 from vqa_module import Layer
@@ -91,22 +92,28 @@ class DecoderConvBlock(Layer):
                                            self.stride))
         return self.output_dim
 
-    def forward(self, x, save=False):
+    def forward(self, x, save=False, stop_before_last_up=False):
+        """stop_before_last_up: return the input of the last up conv (the Decoder runs that conv fused with
+        its output conv, vqa_dtail)."""
         ins = [x]
         x = self.pre.forward(x, self.cdt)
-        for res, up in zip(self.res, self.up):
+        for i, (res, up) in enumerate(zip(self.res, self.up)):
             x = res.forward(x, save)
             ins.append(x)
+            if stop_before_last_up and i == self.down_depth - 1:
+                break
             x = up.forward(x, self.cdt)
         self._saved = ins if save else None
         return x
 
-    def backward(self, dy):
+    def backward(self, dy, skip_last_up=False):
+        """skip_last_up: dy is already the gradient of the last up conv's input (fused decoder tail)."""
         ins = self._saved
         self._saved = None
         for i in reversed(range(self.down_depth)):
-            self.up[i].backward_weight(ins[i + 1], dy, self.cdt)
-            dy = self.up[i].backward_data(dy, self.cdt)
+            if not (skip_last_up and i == self.down_depth - 1):
+                self.up[i].backward_weight(ins[i + 1], dy, self.cdt)
+                dy = self.up[i].backward_data(dy, self.cdt)
             dy = self.res[i].backward(dy)
         self.pre.backward_weight(ins[0], dy, self.cdt)
         return self.pre.backward_data(dy, ins[0].shape[1], self.cdt)
@@ -161,16 +168,47 @@ class Decoder(Layer):
         self.out = Conv1D(store, f"{prefix}/out", dim, self.output_dim, 3)
         return self.output_dim
 
+    # run the last up conv and the output conv as one composed thin conv (vqa_dtail.hip) when they fit it
+    fuse_tail = True
+
+    def _tail(self):
+        up = self.blocks[-1].up[-1]
+        out = self.out
+        ok = (self.fuse_tail and out.cin == up.cout and out.s == 1 and out.d == 1 and
+              V.dtail_supported(up.cin, up.cout, up.K, up.s, out.K, out.cout, V.dtype_code(self.cdt)))
+        return (up, out) if ok else None
+
     def forward(self, x, save=False):
-        for blk in self.blocks:
-            x = blk.forward(x, save)
+        tail = self._tail()
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
+            x = blk.forward(x, save, stop_before_last_up=tail is not None and i == last)
+        if tail is not None:
+            up, out = tail
+            B, T, _ = x.shape
+            y = torch.empty((B, 2 * T, 1), dtype=torch.float32, device=x.device)
+            V.dtail_fwd(x, up.w, up.b, out.w, out.b, y)  # encdec.py:67-68 + :148 composed
+            self._saved = ("tail", x) if save else None
+            return y
         self._saved = x if save else None
         return self.out.forward(x, self.cdt, out_dtype=torch.float32)
 
     def backward(self, dy):
-        x = self._saved
+        saved = self._saved
         self._saved = None
-        g = self.out.backward_data_weight(dy, x, self.cdt)  # one pass: dx and dW/db (vqa_conv_ends.hip)
+        if isinstance(saved, tuple):
+            h = saved[1]
+            up, out = self._tail()
+            g = torch.empty_like(h)
+            st = self.store
+            V.dtail_bwd(dy.contiguous(), h, up.w, up.b, out.w, out.b, g, st.grad_view(f"{up.name}/kernel"),
+                        st.grad_view(f"{up.name}/bias"), st.grad_view(f"{out.name}/kernel"),
+                        st.grad_view(f"{out.name}/bias"))
+            last = len(self.blocks) - 1
+            for i in reversed(range(len(self.blocks))):
+                g = self.blocks[i].backward(g, skip_last_up=(i == last))
+            return g
+        g = self.out.backward_data_weight(dy, saved, self.cdt)  # one pass: dx and dW/db (vqa_conv_ends.hip)
         for blk in reversed(self.blocks):
             g = blk.backward(g)
         return g

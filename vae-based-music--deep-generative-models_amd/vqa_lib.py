@@ -32,7 +32,7 @@ EXPORTED = [
     "vqa_vq_argmin_split", "vqa_vq_split_bf16x3",
     "vqa_resblock_supported", "vqa_resblock_fwd", "vqa_resblock_bwd", "vqa_resblock_bwd_workspace",
     "vqa_spectral_target_workspace", "vqa_spectral_target", "vqa_spectral_loss_target_workspace",
-    "vqa_spectral_loss_target",
+    "vqa_spectral_loss_target", "vqa_dtail_supported", "vqa_dtail_workspace", "vqa_dtail_fwd", "vqa_dtail_bwd",
 ]
 
 
@@ -90,6 +90,10 @@ _SIGS = {
     "vqa_resblock_fwd": (_I, [_P] * 7 + [_I] * 5 + [_P]),
     "vqa_resblock_bwd": (_I, [_P] * 11 + [_I] * 5 + [_P, _S, _P, _P]),
     "vqa_resblock_bwd_workspace": (_S, [_I] * 5),
+    "vqa_dtail_supported": (_I, [_I] * 7),
+    "vqa_dtail_workspace": (_S, [_I] * 5),
+    "vqa_dtail_fwd": (_I, [_P] * 6 + [_I] * 5 + [_P, _S, _P]),
+    "vqa_dtail_bwd": (_I, [_P] * 11 + [_I] * 5 + [_P, _S, _P]),
     "vqa_spectral_target_workspace": (_S, [_I, _I, _P, _P, _P, _I]),
     "vqa_spectral_target": (_I, [_P, _P, _S, _I, _I, _P, _P, _P, _I, _P]),
     "vqa_spectral_loss_target_workspace": (_S, [_I, _I, _P, _P, _P, _I, _I]),
@@ -225,6 +229,32 @@ def conv1d_bwd_data_weight(dy, w, x, residual, dx, dw, db, B, T_in, T_out, C_in,
                                             stream()), "vqa_conv1d_bwd_data_weight")
     if deferred is not None:
         deferred.add(d, ws)
+
+
+def dtail_supported(C, Cu, K_up, stride_up, K_out, C_out, dtype) -> bool:
+    return bool(lib().vqa_dtail_supported(C, Cu, K_up, stride_up, K_out, C_out, dtype))
+
+
+def dtail_fwd(h, w_up, b_up, w_out, b_out, y):
+    """encdec.py:67-68 (last Conv1DTranspose) + :148 (output Conv1D) composed: h (B, T, 32) -> y (B, 2T, 1)
+    fp32 (vqa_dtail_fwd)."""
+    B, T, C = h.shape
+    dt = dtype_code(h.dtype)
+    Cu = w_up.shape[1]
+    ws = workspace(lib().vqa_dtail_workspace(B, T, C, Cu, dt), h.device)
+    _check(lib().vqa_dtail_fwd(ptr(h), ptr(w_up), ptr(b_up), ptr(w_out), ptr(b_out), ptr(y), B, T, C, Cu, dt, ptr(ws),
+                               ws.numel(), stream()), "vqa_dtail_fwd")
+
+
+def dtail_bwd(dy, h, w_up, b_up, w_out, b_out, dh, dw_up, db_up, dw_out, db_out):
+    """Backward of dtail_fwd: dh and the gradients of both layers' kernels and biases (written)."""
+    B, T, C = h.shape
+    dt = dtype_code(h.dtype)
+    Cu = w_up.shape[1]
+    ws = workspace(lib().vqa_dtail_workspace(B, T, C, Cu, dt), h.device)
+    _check(lib().vqa_dtail_bwd(ptr(dy), ptr(h), ptr(w_up), ptr(b_up), ptr(w_out), ptr(b_out), ptr(dh), ptr(dw_up),
+                               ptr(db_up), ptr(dw_out), ptr(db_out), B, T, C, Cu, dt, ptr(ws), ws.numel(), stream()),
+           "vqa_dtail_bwd")
 
 
 def resblock_supported(C, dilation, dtype) -> bool:
