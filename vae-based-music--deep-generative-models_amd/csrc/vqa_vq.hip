@@ -4,7 +4,8 @@
 //   get_code_indices :170-186  -> vq_argmin_mfma_kernel (fp32 MFMA distance tiles + wave argmin);
 //                                 no N x K distance matrix is materialised.
 //   one_hot @ E^T    :86-90    -> a row gather from ET = E^T (K, D) kept by the EMA kernel.
-//   commit loss      :97-99, straight-through :114, EMA sums :123-124 -> vq_quantize_kernel.
+//   commit loss      :97-99, straight-through :114 -> vq_quantize_kernel; EMA sums :123-124 ->
+//                                 vq_ema_sums_kernel (per-chunk LDS tables + a fixed-order reduction).
 //   EMA + dead-code reset :126-145, metrics :149-159 -> vq_ema_apply_kernel / vq_metrics_kernel.
 // The reset candidates (tf.random.shuffle, :137) use an injected, seeded Feistel permutation.
 #include "vqa_common.h"
@@ -412,6 +413,76 @@ static int quantize_blocks(long long total) {
   return (int)b;
 }
 
+// ---- EMA sums by code (VectorQuantizer.py:123-124: m_sum = z^T onehot, n_sum = column sums of onehot) ----
+// A per-row global atomic scatter serialises on the codes a batch crowds into (float atomics execute at the
+// memory side). Instead each workgroup owns a chunk of rows and a 16-channel slice and accumulates
+// [K][16] (+ the counts, slice 0) in LDS with LDS atomics; the chunk partials are then summed in a fixed
+// order by vqa_reduce_partials. Counts are exact; the channel sums are fp32 (LDS atomic order within a
+// chunk is not fixed, as with the global atomics this replaces).
+constexpr int kEmaSlice = 16;
+constexpr int kEmaChunks = 64;
+static bool ema_lds_ok(int D, int K) { return D % kEmaSlice == 0 && (size_t)K * (kEmaSlice + 1) * 4 <= 160 * 1024; }
+static int ema_chunks(long long N) {
+  long long c = (N + 4095) / 4096;
+  return (int)(c < kEmaChunks ? (c > 0 ? c : 1) : kEmaChunks);
+}
+
+constexpr int kEmaThreads = 1024;
+template <class T>
+__global__ __launch_bounds__(kEmaThreads) void vq_ema_sums_kernel(const T* z, const int64_t* idx, float* part, int N, int D,
+                                                          int K, int rows_per_chunk) {
+  extern __shared__ float tab[];  // [K][16] channel sums, then [K] counts
+  float* cnt = tab + K * kEmaSlice;
+  const int chunk = blockIdx.x, slice = blockIdx.y;
+  const bool counts = slice == 0;
+  const int nt = K * kEmaSlice + (counts ? K : 0);
+  for (int i = threadIdx.x; i < nt; i += kEmaThreads) tab[i] = 0.f;
+  __syncthreads();
+  constexpr int RP = kEmaThreads / kEmaSlice;  // rows per pass
+  const int dl = threadIdx.x & (kEmaSlice - 1), rr = threadIdx.x / kEmaSlice;
+  const int r0 = chunk * rows_per_chunk, r1 = min(N, r0 + rows_per_chunk);
+  // each thread keeps a run (code, sum, count) in registers and adds it to the table only when the code
+  // changes: rows crowding into one code cost one LDS atomic per run, not per row
+  constexpr int U = 8;
+  int ck = -1;
+  float cs = 0.f, cc = 0.f;
+  for (int r = r0 + rr; r < r1; r += RP * U) {
+    int k[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ru = r + RP * u;
+      k[u] = ru < r1 ? (int)idx[ru] : -1;
+      v[u] = ru < r1 ? ld(z + (size_t)ru * D + slice * kEmaSlice + dl) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k[u] >= 0) {
+        if (k[u] != ck) {
+          if (ck >= 0) {
+            atomicAdd(tab + ck * kEmaSlice + dl, cs);
+            if (counts && dl == 0) atomicAdd(cnt + ck, cc);
+          }
+          ck = k[u];
+          cs = 0.f;
+          cc = 0.f;
+        }
+        cs += v[u];
+        cc += 1.f;
+      }
+  }
+  if (ck >= 0) {
+    atomicAdd(tab + ck * kEmaSlice + dl, cs);
+    if (counts && dl == 0) atomicAdd(cnt + ck, cc);
+  }
+  __syncthreads();
+  float* out = part + (size_t)chunk * ((size_t)K * D + K);
+  for (int e = threadIdx.x; e < K * kEmaSlice; e += kEmaThreads)
+    out[(size_t)(e / kEmaSlice) * D + slice * kEmaSlice + (e % kEmaSlice)] = tab[e];
+  if (counts)
+    for (int e = threadIdx.x; e < K; e += kEmaThreads) out[(size_t)K * D + e] = cnt[e];
+}
+
 }  // namespace vqa
 
 using namespace vqa;
@@ -477,9 +548,9 @@ extern "C" int vqa_vq_argmin_split(const void* z, const void* E3, const float* e
 }
 
 extern "C" size_t vqa_vq_quantize_workspace(int64_t N, int D, int K, int dtype) {
-  (void)K;
   (void)dtype;
-  return (size_t)quantize_blocks((long long)N * D) * sizeof(float);
+  const size_t head = ((size_t)quantize_blocks((long long)N * D) * sizeof(float) + 255) & ~(size_t)255;
+  return head + (ema_lds_ok(D, K) ? (size_t)ema_chunks(N) * ((size_t)K * D + K) * sizeof(float) : 0);
 }
 
 extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* idx, void* q_st, float* commit_out,
@@ -489,17 +560,48 @@ extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* id
   VQA_ARG(!m_sumT == !n_sum, "vq_quantize: m_sumT and n_sum must both be set or both NULL");
   VQA_ARG(N > 0 && D > 0 && K > 0, "vq_quantize: bad shape");
   const int nb = quantize_blocks((long long)N * D);
-  VQA_ARG(workspace && ws_bytes >= (size_t)nb * sizeof(float), "vq_quantize: workspace too small");
+  VQA_ARG(dtype == VQA_BF16 || dtype == VQA_F32, "vq_quantize: unknown dtype %d", dtype);
+  VQA_ARG(N < (1ll << 31) && D <= 64, "vq_quantize: N=%lld D=%d out of range", (long long)N, D);
+  VQA_ARG(workspace && ws_bytes >= vqa_vq_quantize_workspace(N, D, K, dtype), "vq_quantize: workspace too small");
   hipStream_t s = (hipStream_t)stream;
+  // q, straight-through output and the commitment partials; EMA sums here only when they do not fit the
+  // LDS-table path below
+  const bool lds = m_sumT && ema_lds_ok(D, K);
+  float* ms = lds ? nullptr : m_sumT;
+  float* ns = lds ? nullptr : n_sum;
   if (dtype == VQA_BF16)
-    hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st,
-                       m_sumT, n_sum, (long long)N, D, (float*)workspace);
-  else if (dtype == VQA_F32)
-    hipLaunchKernelGGL(vq_quantize_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)z, ET, idx, (float*)q_st,
-                       m_sumT, n_sum, (long long)N, D, (float*)workspace);
+    hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st, ms,
+                       ns, (long long)N, D, (float*)workspace);
   else
-    VQA_ARG(false, "vq_quantize: unknown dtype %d", dtype);
+    hipLaunchKernelGGL(vq_quantize_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)z, ET, idx, (float*)q_st,
+                       ms, ns, (long long)N, D, (float*)workspace);
   VQA_LAUNCHED("vq_quantize_kernel");
+  if (lds) {
+    const int nch = ema_chunks(N), rpc = (int)((N + nch - 1) / nch);
+    float* part = (float*)((char*)workspace + (((size_t)nb * sizeof(float) + 255) & ~(size_t)255));
+    const size_t lds_bytes = (size_t)K * (kEmaSlice + 1) * sizeof(float);
+    const void* fn = dtype == VQA_BF16 ? (const void*)vq_ema_sums_kernel<bf16> : (const void*)vq_ema_sums_kernel<float>;
+    static size_t lds_set[2] = {0, 0};
+    size_t& cached = lds_set[dtype == VQA_BF16 ? 0 : 1];
+    if (lds_bytes > 65536 && lds_bytes > cached) {
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("vq_quantize: cannot reserve %zu B of LDS", lds_bytes);
+        return VQA_E_UNSUPPORTED;
+      }
+      cached = lds_bytes;
+    }
+    const dim3 grid(nch, D / kEmaSlice);
+    if (dtype == VQA_BF16)
+      hipLaunchKernelGGL(vq_ema_sums_kernel<bf16>, grid, dim3(kEmaThreads), lds_bytes, s, (const bf16*)z, idx, part, (int)N, D,
+                         K, rpc);
+    else
+      hipLaunchKernelGGL(vq_ema_sums_kernel<float>, grid, dim3(kEmaThreads), lds_bytes, s, (const float*)z, idx, part, (int)N,
+                         D, K, rpc);
+    VQA_LAUNCHED("vq_ema_sums_kernel");
+    const vqa_partials_desc d{part, m_sumT, n_sum, nch, K * D + K, K * D, 0};
+    if (int rc = vqa_reduce_partials(&d, 1, stream)) return rc;
+  }
   // beta * mean((q - z)^2) over N*D elements (VectorQuantizer.py:97-99)
   const float scale = (float)((double)beta / ((double)N * (double)D));
   hipLaunchKernelGGL(reduce_scalar_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, scale, commit_out);
