@@ -9,6 +9,7 @@
 //   EMA + dead-code reset :126-145, metrics :149-159 -> vq_ema_apply_kernel / vq_metrics_kernel.
 // The reset candidates (tf.random.shuffle, :137) use an injected, seeded Feistel permutation.
 #include "vqa_common.h"
+#include <algorithm>
 
 namespace vqa {
 
@@ -125,9 +126,27 @@ __global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const f
 // WG = 4 waves x 64 rows; code chunks of KC codes (3 planes, padded rows) staged in LDS.
 constexpr int kSplitKC = 64;
 
+// (distance, index) -> one uint64 whose unsigned order is (distance, then index): the K-split partial results
+// combine with atomicMin in any order to the same winner (ties -> lowest index, as tf.argmin)
+__device__ __forceinline__ unsigned long long vq_pack(float d, int k) {
+  unsigned u = __float_as_uint(d);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned)k;
+}
+__device__ __forceinline__ float vq_unpack_dist(unsigned long long p) {
+  unsigned u = (unsigned)(p >> 32);
+  u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  return __uint_as_float(u);
+}
+
+// blockIdx.y = code split: codes [y*kspan, (y+1)*kspan); with more than one split the row results go to
+// idx as packed keys through atomicMin (vq_argmin_unpack_kernel turns them into indices / distances)
 template <int D>
 __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, const bf16* E3, const float* esq,
-                                                             int64_t* idx, float* mind, long long N, int K) {
+                                                             int64_t* idx, float* mind, long long N, int K,
+                                                             int kspan) {
+  const int kbeg = blockIdx.y * kspan, kend = min(K, kbeg + kspan);
+  const bool packed = gridDim.y > 1;
   constexpr int KC = kSplitKC, KS = D / 32, RT = 4;
   constexpr int CS = 3 * D + 8;          // LDS code stride (bf16): +16 B so 16 codes hit distinct banks
   constexpr int PPC = 3 * D * 2 / 16;    // 16-byte pieces per code
@@ -174,15 +193,15 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
       bidx[rt][r] = 0x7fffffff;
     }
 
-  for (int k0 = 0; k0 < K; k0 += KC) {
+  for (int k0 = kbeg; k0 < kend; k0 += KC) {
     __syncthreads();
     for (int e = threadIdx.x; e < KC * PPC; e += 256) {
       const int c = e / PPC, p = e - c * PPC;
       uint4 v = {0u, 0u, 0u, 0u};
-      if (k0 + c < K) v = *(const uint4*)(E3 + (size_t)(k0 + c) * 3 * D + p * 8);
+      if (k0 + c < kend) v = *(const uint4*)(E3 + (size_t)(k0 + c) * 3 * D + p * 8);
       *(uint4*)(El + c * CS + p * 8) = v;
     }
-    for (int e = threadIdx.x; e < KC; e += 256) el2[e] = (k0 + e < K) ? esq[k0 + e] : 0.f;
+    for (int e = threadIdx.x; e < KC; e += 256) el2[e] = (k0 + e < kend) ? esq[k0 + e] : 0.f;
     __syncthreads();
 #pragma unroll 1
     for (int ct = 0; ct < KC / 16; ++ct) {
@@ -207,7 +226,7 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
         for (int r = 0; r < 4; ++r) {
           const float t = zq[rt][r] + e2;
           const float dist = t - 2.0f * acc[r];
-          if (kg < K && dist < best[rt][r]) {
+          if (kg < kend && dist < best[rt][r]) {
             best[rt][r] = dist;
             bidx[rt][r] = kg;
           }
@@ -232,10 +251,26 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
       }
       const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
       if ((lane & 15) == 0 && row < N) {
-        idx[row] = bi;
-        if (mind) mind[row] = b;
+        if (packed) {
+          if (bi != 0x7fffffff) atomicMin((unsigned long long*)idx + row, vq_pack(b, bi));
+        } else {
+          idx[row] = bi;
+          if (mind) mind[row] = b;
+        }
       }
     }
+}
+
+__global__ __launch_bounds__(256) void vq_argmin_init_kernel(int64_t* idx, long long N) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < N) idx[i] = (int64_t)~0ull;
+}
+__global__ __launch_bounds__(256) void vq_argmin_unpack_kernel(int64_t* idx, float* mind, long long N) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  const unsigned long long p = (unsigned long long)idx[i];
+  idx[i] = (int64_t)(unsigned)(p & 0xffffffffu);
+  if (mind) mind[i] = vq_unpack_dist(p);
 }
 
 // E (D, K) fp32 -> E3 (K, 3, D) bf16 planes with hi + mid + lo = E
@@ -535,15 +570,29 @@ extern "C" int vqa_vq_argmin_split(const void* z, const void* E3, const float* e
   VQA_ARG(z && E3 && e_sqnorm && idx, "vq_argmin_split: null pointer");
   VQA_ARG(N > 0 && K > 0 && (D == 32 || D == 64), "vq_argmin_split: bad shape N=%lld D=%d K=%d (D in {32, 64})",
           (long long)N, D, K);
-  const dim3 g((unsigned)((N + 255) / 256));
+  // rows blocks of 256; small batches also split the codebook so that >= ~512 workgroups run
+  const long long rb = (N + 255) / 256;
+  int nsplit = (int)std::min<long long>(std::max<long long>(1, 512 / rb), (K + kSplitKC - 1) / kSplitKC);
+  const int kspan = ((K + nsplit - 1) / nsplit + kSplitKC - 1) / kSplitKC * kSplitKC;
+  nsplit = (K + kspan - 1) / kspan;
+  const dim3 g((unsigned)rb, (unsigned)nsplit);
   hipStream_t s = (hipStream_t)stream;
+  const unsigned nb = (unsigned)((N + 255) / 256);
+  if (nsplit > 1) {
+    hipLaunchKernelGGL(vq_argmin_init_kernel, dim3(nb), dim3(256), 0, s, idx, (long long)N);
+    VQA_LAUNCHED("vq_argmin_init_kernel");
+  }
   if (D == 64)
     hipLaunchKernelGGL(vq_argmin_split_kernel<64>, g, dim3(256), 0, s, (const bf16*)z, (const bf16*)E3, e_sqnorm, idx,
-                       min_dist, (long long)N, K);
+                       min_dist, (long long)N, K, kspan);
   else
     hipLaunchKernelGGL(vq_argmin_split_kernel<32>, g, dim3(256), 0, s, (const bf16*)z, (const bf16*)E3, e_sqnorm, idx,
-                       min_dist, (long long)N, K);
+                       min_dist, (long long)N, K, kspan);
   VQA_LAUNCHED("vq_argmin_split_kernel");
+  if (nsplit > 1) {
+    hipLaunchKernelGGL(vq_argmin_unpack_kernel, dim3(nb), dim3(256), 0, s, idx, min_dist, (long long)N);
+    VQA_LAUNCHED("vq_argmin_unpack_kernel");
+  }
   return VQA_OK;
 }
 
