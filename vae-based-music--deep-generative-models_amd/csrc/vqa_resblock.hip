@@ -220,9 +220,9 @@ template <class T> constexpr int rs_ncc() { return RC / Mfma<T>::KS; }
 
 // A fragments of a forward conv held in registers: wf[k][mt][cc-step] (A[m][K] = W[k][c][och(mt, m)],
 // Keras layout), loaded once per workgroup
-template <class T>
+template <class T, bool KPERM>
 __device__ __forceinline__ void load_wfrags(typename Mfma<T>::frag (&wf)[3][2][rs_ncc<T>()], const float* w) {
-  const int lane = threadIdx.x & 63, m = lane & 15, kc = rs_kcol<T, false>(lane);
+  const int lane = threadIdx.x & 63, m = lane & 15, kc = rs_kcol<T, KPERM>(lane);
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -295,6 +295,8 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o
 
 // ---------------------------------------------------------------------------------------------------
 // 3 waves/SIMD for bf16 (<= 168 VGPRs without spilling); the fp32 parity build needs more registers
+// forward K order: natural (false) keeps it bit-identical to the unfused gather kernels
+constexpr bool kRsFwdKperm = false;
 template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2; }
 
 template <class T, int DT>
@@ -309,8 +311,8 @@ void resblock_fwd_kernel(ResArgs a) {
   const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
   if (tbeg >= tend) return;
   typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()], wfb[3][2][rs_ncc<T>()];
-  load_wfrags<T>(wfa, a.wa);
-  load_wfrags<T>(wfb, a.wb);
+  load_wfrags<T, kRsFwdKperm>(wfa, a.wa);
+  load_wfrags<T, kRsFwdKperm>(wfb, a.wb);
   const int pn = rs_pi(lane & 15), oc = rs_ocol(lane);
   f32x4 bav[2], bbv[2];
 #pragma unroll
@@ -339,7 +341,7 @@ void resblock_fwd_kernel(ResArgs a) {
       f32x4 acc[3][2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = min(wave + 4 * j, HR / 16 - 1) * 16;
-      conv_multi<T, true, false, false, 3>(acc, wa_frag, X, rb, d);
+      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= HR / 16) continue;
@@ -370,7 +372,7 @@ void resblock_fwd_kernel(ResArgs a) {
       f32x4 acc[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16;
-      conv_multi<T, false, false, false, 2>(acc, wb_frag, H, rb, 1);
+      conv_multi<T, false, kRsFwdKperm, false, 2>(acc, wb_frag, H, rb, 1);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int tl = rb[j] + pn;
