@@ -58,10 +58,12 @@ def parse():
 
 class KernelTimer:
     """Roofline of the dominant kernel, resblock_bwd_kernel<bf16> (resnet.py:7-29 backward, one launch per
-    residual block): record every vqa_resblock_bwd call of one step, then time each distinct call as
-    back-to-back copies inside a hipGraph replayed on the stream libvqa launches on, bracketed by HIP events
-    (no host gaps, so the per-launch average is the kernel's own duration, as rocprofv3 reports it). The
-    weight-gradient partial reduction is left out (its own kernel).
+    residual block): record every vqa_resblock_bwd call of one step (in order, with its own tensors), then
+    capture ALL of them back to back into one hipGraph and time its replays with HIP events on the stream
+    libvqa launches on. One graph for the whole mix amortises the graph-launch overhead over the step's
+    launches, so the per-launch average is the kernels' own duration (plus the ~1 us inter-kernel gap of a
+    graph) and matches rocprofv3's average for the kernel. The weight-gradient partial reduction is left
+    out (its own kernel).
 
     Algorithmic bytes per launch (SURVEY.md §8d layer model): the launch does the data- and
     weight-gradient of the block's two convs, 2 x (|in| + |out|) per conv = 8 activation tensors of
@@ -69,19 +71,15 @@ class KernelTimer:
 
     def __init__(self, V):
         self.V = V
-        self.calls = {}
+        self.calls = []
         self.orig = None
 
     def __enter__(self):
         self.orig = f = self.V.resblock_bwd
 
         def wrapped(dy, x, *rest, _f=f):
-            key = (tuple(x.shape), x.dtype, rest[-2] if len(rest) >= 2 else None, x.data_ptr())
             unit = x.numel() * x.element_size()
-            if key in self.calls:
-                self.calls[key][1] += 1
-            else:
-                self.calls[key] = [(dy, x) + tuple(rest), 1, 8 * unit, 3 * unit]
+            self.calls.append(((dy, x) + tuple(rest), 8 * unit, 3 * unit))
             return _f(dy, x, *rest)
         self.V.resblock_bwd = wrapped
         return self
@@ -90,32 +88,29 @@ class KernelTimer:
         self.V.resblock_bwd = self.orig
 
     def measure(self, reps=5):
-        """-> (launches per step, total us per step, algorithmic bytes per step, compulsory bytes per step).
-        Each distinct launch is replayed as many times per graph as it occurs in a step, so the replays
-        have the step's mix and rocprofv3's average over the whole run stays comparable."""
-        n_launch, us_total, nbytes, cbytes = 0, 0.0, 0, 0
+        """-> (launches per step, total us per step, algorithmic bytes per step, compulsory bytes per step)."""
+        if not self.calls:
+            return 0, 0.0, 0, 0
         stream = torch.cuda.current_stream()
         f = self.orig
-        for key, (args, cnt, nb, cb) in self.calls.items():
-            args = args[:-1] + (self.V.Deferred(),)  # partials left unreduced: time the kernel alone
+        deferred = self.V.Deferred()  # partials left unreduced: time the kernel alone
+        runs = [args[:-1] + (deferred,) for args, _, _ in self.calls]
+        for args in runs:
             f(*args)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(cnt):
-                    f(*args)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for args in runs:
+                f(*args)
+        g.replay()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(reps):
             g.replay()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record(stream)
-            for _ in range(reps):
-                g.replay()
-            e.record(stream)
-            torch.cuda.synchronize()
-            us = s.elapsed_time(e) * 1e3 / (reps * cnt)
-            n_launch += cnt
-            us_total += cnt * us
-            nbytes += cnt * nb
-            cbytes += cnt * cb
-        return n_launch, us_total, nbytes, cbytes
+        e.record(stream)
+        torch.cuda.synchronize()
+        n = len(runs)
+        us_total = s.elapsed_time(e) * 1e3 / reps
+        return n, us_total, sum(c[1] for c in self.calls), sum(c[2] for c in self.calls)
 
 
 def cpu_baseline(batch, steps, seq):

@@ -15,7 +15,7 @@ import os
 import re
 import sys
 
-FAMILY = re.compile(r"resblock_bwd_kernel(IDF16b|<__bf16|<bf16)")
+FAMILY = re.compile(r"resblock_bwd_kernel(IDF16b|<__bf16|<bf16|<bool _Accum)")
 
 
 def per_dispatch(d, counter):

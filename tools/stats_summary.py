@@ -8,7 +8,7 @@ import json
 import re
 import sys
 
-FAMILY = re.compile(r"resblock_bwd_kernel(IDF16b|<__bf16|<bf16)")
+FAMILY = re.compile(r"resblock_bwd_kernel(IDF16b|<__bf16|<bf16|<bool _Accum)")
 rows = list(csv.DictReader(open(sys.argv[1])))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"# rocprofv3 --kernel-trace --stats summary ({sys.argv[1].split('/')[-1]})\n")
