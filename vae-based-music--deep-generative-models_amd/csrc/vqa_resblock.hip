@@ -20,11 +20,12 @@
 #include "vqa_common.h"
 #include "vqa_mfma.h"
 #include <stdlib.h>
+#include <algorithm>
 
 namespace vqa {
 
 constexpr int RC = 32;    // block width (residual_width of the SMALL_VQ_VAE configs)
-constexpr int RTM = 128;  // output rows per tile
+constexpr int RTM = 128;  // output rows per tile (runtime-dilation kernels; see rs_fwd_rt / rs_bwd_rt)
 constexpr int RMAXD = 32; // largest dilation the LDS plan covers (the model uses 1, 3, 9, 27)
 
 struct ResArgs {
@@ -299,10 +300,16 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o
 constexpr bool kRsFwdKperm = false;
 template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2; }
 
-template <class T, int DT>
+// Rows per tile: chosen so that the recomputed rows fill whole 16-row MFMA tiles over the 4 waves
+// (forward: RT + 16 = 192 = 12 tiles; backward: round16(RT + 2d) <= 192 with RT a multiple of 32 for the
+// K = rows weight-gradient products)
+constexpr int rs_fwd_rt(int dt) { return dt > 0 ? 176 : RTM; }
+constexpr int rs_bwd_rt(int dt) { return (dt > 0 && dt <= 9) ? 160 : RTM; }
+
+template <class T, int DT, int RT = rs_fwd_rt(DT)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_fwd_waves<T>(), 8)))
 void resblock_fwd_kernel(ResArgs a) {
-  constexpr int XS = rs_stride<T>(), HR = RTM + 16;
+  constexpr int XS = rs_stride<T>(), HR = RT + 16, NT = RT / 16, NJ = (NT + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* X = (T*)smem;  // local j <-> row t0 - 1 - d + j, XR = HR + 2d rows (raw x)
   const int d = DT > 0 ? DT : a.d, XR = HR + 2 * d;
@@ -322,7 +329,7 @@ void resblock_fwd_kernel(ResArgs a) {
   }
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
   auto item_x = [&](int tile) { return rs_rsrc((const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC, ibytes); };
-  auto row0 = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RTM - 1 - d; };
+  auto row0 = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RT - 1 - d; };
   Rows32Buf<T, rs_pv<T>()> nx;
   nx.init(XR);
   nx.load(item_x(tbeg), row0(tbeg));
@@ -330,13 +337,13 @@ void resblock_fwd_kernel(ResArgs a) {
   if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1));
   __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
-    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
-    // h rows t0-1 .. t0+142 (conv_b reads t0-1 .. t0+128); rows outside the item are conv_b's SAME zeros
+    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RT;
+    // h rows t0-1 .. t0+RT+14 (conv_b reads t0-1 .. t0+RT); rows outside the item are conv_b's SAME zeros
     const bool interior = t0 - 1 >= 0 && t0 - 1 + HR <= a.T;  // uniform: no SAME-padding rows in h
     auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
     auto wb_frag = [&](int k, int mt, int sc) { return wfb[k][mt][sc]; };
     {
-      // h n-tiles wave, wave+4, wave+8 of HR/16 = 9 (an out-of-range slot computes a valid tile, unstored)
+      // h n-tiles wave, wave+4, wave+8 of HR/16 (an out-of-range slot computes a valid tile, unstored)
       int rb[3];
       f32x4 acc[3][2];
 #pragma unroll
@@ -360,21 +367,22 @@ void resblock_fwd_kernel(ResArgs a) {
           }
         }
         st8(H + i * XS + oc, v[0], v[1]);
-        // the tile's own rows 1..RTM (rows >= T dropped by the range check)
-        if (a.h && i >= 1 && i <= RTM)
+        // the tile's own rows 1..RT (rows >= T dropped by the range check)
+        if (a.h && i >= 1 && i <= RT)
           st8_buf<T>(rs_rsrc((T*)a.h + (size_t)n * a.T * RC, ibytes), (r * RC + oc) * (int)sizeof(T), v[0], v[1]);
       }
     }
     __syncthreads();
     {
       const __amdgpu_buffer_rsrc_t yr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
-      int rb[2];
-      f32x4 acc[2][2];
+      int rb[NJ];
+      f32x4 acc[NJ][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16;
-      conv_multi<T, false, kRsFwdKperm, false, 2>(acc, wb_frag, H, rb, 1);
+      for (int j = 0; j < NJ; ++j) rb[j] = min(wave + 4 * j, NT - 1) * 16;
+      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, rb, 1);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
+        if (wave + 4 * j >= NT) continue;
         const int tl = rb[j] + pn;
         f32x4 x0, x1;
         ld8(X + (tl + 1 + d) * XS + oc, x0, x1);
@@ -393,12 +401,12 @@ void resblock_fwd_kernel(ResArgs a) {
 // ---------------------------------------------------------------------------------------------------
 // DT > 0: the dilation as a compile-time constant (every LDS offset of the tile becomes an immediate);
 // DT = 0: any dilation <= RMAXD from the arguments
-template <class T, int DT>
+template <class T, int DT, int RT = rs_bwd_rt(DT)>
 __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
-  constexpr int WS = rs_stride<T>(), XS = WS;
+  constexpr int WS = rs_stride<T>(), XS = WS, NT = RT / 16, NJ = (NT + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int d = DT > 0 ? DT : a.d, HR = round16(RTM + 2 * d), XR = HR + 2 * d, YR = HR + 2;
+  const int d = DT > 0 ? DT : a.d, HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
   T* waF = (T*)smem;            // conv_a forward (recompute h): output o, input c
   T* waT = waF + 3 * RC * WS;   // conv_a^T: output c, input o
   T* wbT = waT + 3 * RC * WS;   // conv_b^T: output c, input o
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
 
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
   auto item_off = [&](int tile) { return (size_t)(tile / a.ntm) * a.T * RC; };
-  auto tstart = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RTM; };
+  auto tstart = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RT; };
   auto load_tile = [&](Rows32Buf<T, rs_pv<T>()>& bx, Rows32Buf<T, rs_pv<T>()>& by, int tile) {
     const size_t o = item_off(tile);
     bx.load(rs_rsrc((const T*)a.x + o, ibytes), tstart(tile) - 2 * d);
@@ -448,7 +456,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   if (tbeg + 1 < tend) load_tile(nx, ny, tbeg + 1);
   __syncthreads();
   for (int tile = tbeg; tile < tend; ++tile) {
-    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RTM;
+    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RT;
     // 1. recompute relu(h) over the dh rows (zero outside the item)
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
     int rh[3];
@@ -481,7 +489,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     // 2a. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o], db_b += sum_t dy[t] (the tile's own rows)
     if (!(a.skip & 2)) {
 #pragma unroll
-      for (int kk = 0; kk < RTM; kk += M::KS) {
+      for (int kk = 0; kk < RT; kk += M::KS) {
         const typename M::frag bf = rs_rows(Y + (d + 1 + kk) * XS + ot * 16, XS);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -521,13 +529,14 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows
     if (!(a.skip & 8)) {
       const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + item_off(tile), ibytes);
-      int rb[2];
-      f32x4 acc[2][2];
+      int rb[NJ];
+      f32x4 acc[NJ][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) rb[j] = (wave + 4 * j) * 16 + 2 * d;
-      conv_multi<T, false, true, true, 2>(acc, img_frag(waT), H, rb, -d);
+      for (int j = 0; j < NJ; ++j) rb[j] = min(wave + 4 * j, NT - 1) * 16 + 2 * d;
+      conv_multi<T, false, true, true, NJ>(acc, img_frag(waT), H, rb, -d);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
+        if (wave + 4 * j >= NT) continue;
         const int tl = (wave + 4 * j) * 16 + pn;
         bool xp[8];
         f32x4 y0, y1;
@@ -544,7 +553,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     // 4. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o], db_a += sum_t dh[t]
     if (!(a.skip & 16)) {
 #pragma unroll
-      for (int kk = 0; kk < RTM; kk += M::KS) {
+      for (int kk = 0; kk < RT; kk += M::KS) {
         const typename M::frag bf = rs_rows(H + (d + kk) * XS + ot * 16, XS);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -592,12 +601,12 @@ static int rs_cus() {
 }
 constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the partial rows)
 
-static size_t fwd_lds(int d, int esz) {
-  const int s = RC + 16 / esz, HR = RTM + 16;
+static size_t fwd_lds(int d, int esz, int rt) {
+  const int s = RC + 16 / esz, HR = rt + 16;
   return ((size_t)(HR + 2 * d) * s + (size_t)HR * s) * esz;
 }
-static size_t bwd_lds(int d, int esz) {
-  const int s = RC + 16 / esz, HR = round16(RTM + 2 * d);
+static size_t bwd_lds(int d, int esz, int rt) {
+  const int s = RC + 16 / esz, HR = round16(rt + 2 * d);
   return ((size_t)9 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
 }
 
@@ -636,8 +645,11 @@ template <class F> static const void* rs_pick(int d) {
   }
 }
 
-static void plan(ResArgs& a, int per_cu) {
-  a.ntm = (a.T + RTM - 1) / RTM;
+static int fwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_fwd_rt(d) : RTM; }
+static int bwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_bwd_rt(d) : RTM; }
+
+static void plan(ResArgs& a, int per_cu, int rt) {
+  a.ntm = (a.T + rt - 1) / rt;
   a.ntiles = a.ntm * a.B;
   int nwg = rs_cus() * per_cu;
   if (nwg > a.ntiles) nwg = a.ntiles;
@@ -651,7 +663,8 @@ using namespace vqa;
 extern "C" int vqa_resblock_supported(int C, int dilation, int dtype) {
   if (C != RC || dilation < 1 || dilation > RMAXD || !(dtype == VQA_F32 || dtype == VQA_BF16)) return 0;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
-  return bwd_lds(dilation, esz) <= 160 * 1024 && fwd_lds(dilation, esz) <= 160 * 1024;
+  return bwd_lds(dilation, esz, bwd_rt_of(dilation)) <= 160 * 1024 &&
+         fwd_lds(dilation, esz, fwd_rt_of(dilation)) <= 160 * 1024;
 }
 
 extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba, const float* wb, const float* bb,
@@ -662,9 +675,10 @@ extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba,
               "resblock_fwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
   VQA_ARG((long long)T * C * 4 < (1ll << 30), "resblock_fwd: item too long for 32-bit buffer offsets (T=%d)", T);
   ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0, 0};
-  plan(a, 3);
+  plan(a, 3, fwd_rt_of(dilation));
   const int esz = dtype == VQA_BF16 ? 2 : 4;
-  const size_t lds = fwd_lds(RMAXD, esz);  // one LDS reservation for every dilation
+  // one LDS reservation for every dilation (the largest plan)
+  const size_t lds = std::max(fwd_lds(RMAXD, esz, RTM), fwd_lds(27, esz, rs_fwd_rt(27)));
   const hipStream_t s = (hipStream_t)stream;
   const dim3 grid((a.ntiles + a.tpw - 1) / a.tpw);
   const void* fn = dtype == VQA_BF16 ? rs_pick<RsFwd<bf16>>(dilation) : rs_pick<RsFwd<float>>(dilation);
@@ -701,12 +715,12 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
     return e ? atoi(e) : 0;
   }();
   a.skip = dbg_skip;
-  plan(a, kResPerCU);
+  plan(a, kResPerCU, bwd_rt_of(dilation));
   const int nwg = (a.ntiles + a.tpw - 1) / a.tpw;
   a.part_b = a.part_a + (size_t)nwg * E;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
-  const size_t lds = bwd_lds(dilation, esz);
-  const size_t lds_max = bwd_lds(RMAXD, esz);
+  const size_t lds = bwd_lds(dilation, esz, bwd_rt_of(dilation));
+  const size_t lds_max = std::max(bwd_lds(RMAXD, esz, RTM), bwd_lds(9, esz, rs_bwd_rt(9)));
   const hipStream_t s = (hipStream_t)stream;
   const void* fn = dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation);
   if (int rc = set_lds(fn, lds_max)) return rc;
