@@ -92,15 +92,13 @@ __device__ __forceinline__ f32x2* fft(f32x2* a, f32x2* b, const f32x2* tw, int l
   return (fft_stages<N>() & 1) ? b : a;
 }
 
-enum { SPEC_GRAD = 0, SPEC_LOSS = 1, SPEC_MAG = 2 };
 constexpr int SPEC_MAX_RES = 8;
 
+// |STFT| of a signal (vqa_stft_magnitude: no workspace, so the twiddles and window are evaluated in the
+// kernel when tw is null)
 struct SpecFrameArgs {
-  const float* x;   // target (B, T) fp32
-  const float* r;   // reconstruction (B, T) fp32 (unused for SPEC_MAG)
-  float* fg;        // SPEC_GRAD: unscaled frame gradients (B*F, win)
-  float* part;      // SPEC_GRAD/LOSS: per-frame (sum (|X|-|R|)^2, sum |X|^2)
-  float* mag;       // SPEC_MAG: |X| (B*F, N/2+1)
+  const float* x;   // signal (B, T) fp32
+  float* mag;       // |X| (B*F, N/2+1)
   const float* tw;  // N twiddles (re, im) from spec_tables_kernel, or null: evaluated in the kernel
   const float* wn;  // periodic Hann window of length win (null with tw)
   int B, T, F, hop, win;
@@ -109,21 +107,19 @@ struct SpecFrameArgs {
 // threads per frame: N/4 butterflies per radix-4 stage, at most the whole workgroup
 template <int N> constexpr int spec_tpf() { return N / 4 < 256 ? N / 4 : 256; }
 
-template <int N, int MODE>
+template <int N>
 __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
   constexpr int TPF = spec_tpf<N>(), FPI = 256 / TPF;  // frame slots per workgroup
-  constexpr int KB = N / 2 + 1, NB = (KB + TPF - 1) / TPF, WPF = TPF / 64;
+  constexpr int KB = N / 2 + 1, NB = (KB + TPF - 1) / TPF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f32x2* tw = (f32x2*)smem;
   float* wn = (float*)(tw + N);
   f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
-  const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF, wave = tid >> 6;
+  const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF;
   f32x2* buf0 = slots + (size_t)sl * 2 * N;
   f32x2* buf1 = buf0 + N;
-  __shared__ float red[2][4];
 
   if (a.tw) {
-    // tables computed once per call (fp64, rounded once): 16-byte copies
     for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
     for (int e = tid; e < a.win; e += 256) wn[e] = a.wn[e];
   } else {
@@ -137,9 +133,8 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
   __syncthreads();
 
   const int nframes = a.B * a.F;
-  // the samples of a frame slot, NL per thread (n = lt + i*TPF), are loaded one frame ahead into registers
   constexpr int NL = N / TPF;
-  float xv[NL], rv[NL];
+  float xv[NL];
   auto load_frame = [&](int f0_) {
     const int fc = min(f0_ + sl, nframes - 1);  // an idle slot recomputes a valid frame and stores nothing
     const int bb = fc / a.F, f = fc - bb * a.F;
@@ -147,122 +142,50 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int n = lt + i * TPF;
-      const int nc = n < a.win ? n : 0;
-      xv[i] = a.x[off + nc];
-      if constexpr (MODE != SPEC_MAG) rv[i] = a.r[off + nc];
+      xv[i] = a.x[off + (n < a.win ? n : 0)];
     }
   };
   if (blockIdx.x * FPI < nframes) load_frame(blockIdx.x * FPI);
   for (int f0 = blockIdx.x * FPI; f0 < nframes; f0 += gridDim.x * FPI) {
     const int fi = f0 + sl;
-    const bool act = fi < nframes;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int n = lt + i * TPF;
       buf0[n] = n < a.win ? f32x2{xv[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
     }
-    float rcur[NL];
-#pragma unroll
-    for (int i = 0; i < NL; ++i) rcur[i] = (MODE != SPEC_MAG) ? rv[i] : 0.f;
-    if (f0 + gridDim.x * FPI < nframes) load_frame(f0 + gridDim.x * FPI);  // lands during this frame's FFTs
+    if (f0 + gridDim.x * FPI < nframes) load_frame(f0 + gridDim.x * FPI);  // lands during this frame's FFT
     __syncthreads();
     const f32x2* X = fft<N, false, TPF>(buf0, buf1, tw, lt);
-    float mx[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int k = lt + TPF * j;
-      mx[j] = k < KB ? cabs2(X[k]) : 0.f;
-    }
-    if constexpr (MODE == SPEC_MAG) {
-      if (act) {
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const int k = lt + TPF * j;
-          if (k < KB) a.mag[(size_t)fi * KB + k] = mx[j];
-        }
-      }
-      __syncthreads();
-      continue;
-    } else {
-      __syncthreads();  // every read of X done before buf0/buf1 are reused
-#pragma unroll
-      for (int i = 0; i < NL; ++i) {
-        const int n = lt + i * TPF;
-        buf0[n] = n < a.win ? f32x2{rcur[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
-      }
-      __syncthreads();
-      f32x2* R = fft<N, false, TPF>(buf0, buf1, tw, lt);
-      f32x2* H = (R == buf0) ? buf1 : buf0;  // free since the last FFT stage's sync
-      float sd = 0.f, sx = 0.f;
+    if (fi < nframes) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int k = lt + TPF * j;
-        if (k < KB) {
-          const f32x2 rk = R[k];
-          const float mr = cabs2(rk), d = mx[j] - mr;
-          sd += d * d;
-          sx += mx[j] * mx[j];
-          if constexpr (MODE == SPEC_GRAD) {
-            // dL/d(Re,Im)R_k = (|R|-|X|) R/|R|; Hermitian extension for the adjoint of the one-sided rfft
-            const float g = mr > 0.f ? (mr - mx[j]) / mr : 0.f;
-            const f32x2 G = f32x2{g * rk.x, g * rk.y};
-            if (k == 0 || k == N / 2) {
-              H[k] = f32x2{G.x, 0.f};
-            } else {
-              H[k] = f32x2{0.5f * G.x, 0.5f * G.y};
-              H[N - k] = f32x2{0.5f * G.x, -0.5f * G.y};
-            }
-          }
-        }
+        if (k < KB) a.mag[(size_t)fi * KB + k] = cabs2(X[k]);
       }
-      // per-slot sums: wave sums, then the slot's waves in a fixed order
-      sd = warp_sum(sd);
-      sx = warp_sum(sx);
-      if ((tid & 63) == 0) {
-        red[0][wave] = sd;
-        red[1][wave] = sx;
-      }
-      __syncthreads();  // also orders the H writes before the inverse FFT
-      if (lt == 0 && act) {
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int w = 0; w < WPF; ++w) {
-          s0 += red[0][sl * WPF + w];
-          s1 += red[1][sl * WPF + w];
-        }
-        a.part[2 * (size_t)fi] = s0;
-        a.part[2 * (size_t)fi + 1] = s1;
-      }
-      if constexpr (MODE == SPEC_GRAD) {
-        f32x2* other = (H == buf0) ? buf1 : buf0;
-        const f32x2* Y = fft<N, true, TPF>(H, other, tw, lt);
-        if (act) {
-          float* out = a.fg + (size_t)fi * a.win;
-          for (int n = lt; n < a.win; n += TPF) out[n] = Y[n].x * wn[n];
-        }
-      }
-      __syncthreads();  // red[] and the slot buffers are reused by the next frames
     }
+    __syncthreads();
   }
 }
 
-// Loss (and gradient) of the reconstruction against PRECOMPUTED target magnitudes |S_x| (the target's STFT
-// is the same for every level of a step, so it is transformed once, by spec_frame_kernel<SPEC_MAG>). A frame
-// slot takes frames in PAIRS (a, b): two forward FFTs of the windowed reconstruction frames, then ONE inverse
-// FFT of H_a + i H_b — both adjoint outputs are real, so y_a = Re, y_b = Im exactly (no cancellation: the
-// forward transforms stay separate). 1.5 FFTs per frame instead of 3.
+// Frames in PAIRS (a, b) per slot: ONE complex FFT of z = w*s_a + i w*s_b gives both real frames' spectra
+// (S_a[k] = (Z[k] + conj Z[N-k]) / 2, S_b[k] = (Z[k] - conj Z[N-k]) / 2i). MAG writes |S| (the target's
+// spectrograms, once per step); LOSS / GRAD compare |S| of the reconstruction against the precomputed
+// target magnitudes and GRAD runs ONE inverse FFT of H_a + i H_b (both adjoint outputs are real, so
+// y_a = Re, y_b = Im). One FFT per frame (two with the gradient) instead of the three of a direct form.
+enum { PAIR_LOSS = 0, PAIR_GRAD = 1, PAIR_MAG = 2 };
 struct SpecPairArgs {
-  const float* r;   // reconstruction (B, T) fp32
-  const float* tm;  // target magnitudes (B*F, N/2+1)
-  float* fg;        // GRAD: unscaled frame gradients (B*F, win)
-  float* part;      // per-frame (sum (|X|-|R|)^2, sum |X|^2)
+  const float* r;   // signal (B, T) fp32: reconstruction (LOSS, GRAD) or target (MAG)
+  const float* tm;  // LOSS / GRAD: target magnitudes (B*F, N/2+1)
+  float* out;       // GRAD: unscaled frame gradients (B*F, win); MAG: magnitudes (B*F, N/2+1)
+  float* part;      // LOSS / GRAD: per-frame (sum (|X|-|R|)^2, sum |X|^2)
   const float* tw;  // N twiddles (re, im)
   const float* wn;  // window
   int B, T, F, hop, win;
 };
 
-template <int N, bool GRAD>
+template <int N, int MODE>
 __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
+  constexpr bool GRAD = MODE == PAIR_GRAD, MAG = MODE == PAIR_MAG;
   constexpr int TPF = spec_tpf<N>(), FPI = 256 / TPF;  // frame-pair slots per workgroup
   constexpr int KB = N / 2 + 1, NB = (KB + TPF - 1) / TPF, WPF = TPF / 64, NL = N / TPF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -270,9 +193,8 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
   float* wn = (float*)(tw + N);
   f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
   const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF, wave = tid >> 6;
-  f32x2* bA = slots + (size_t)sl * 3 * N;
+  f32x2* bA = slots + (size_t)sl * 2 * N;
   f32x2* bB = bA + N;
-  f32x2* bC = bB + N;
   __shared__ float red[4][4];
 
   for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
@@ -280,8 +202,8 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
   __syncthreads();
 
   const int nframes = a.B * a.F, npairs = (nframes + 1) / 2;
-  // samples and target magnitudes of the slot's pair, loaded one pair ahead into registers
-  float ra[NL], rb[NL], ta[NB], tb[NB];
+  // samples (and target magnitudes) of the slot's pair, loaded one pair ahead into registers
+  float ra[NL], rb[NL], ta[MAG ? 1 : NB], tb[MAG ? 1 : NB];
   auto load_pair = [&](int p0) {
     const int pa = min(2 * (p0 + sl), nframes - 1), pb = min(2 * (p0 + sl) + 1, nframes - 1);
     const int ba_ = pa / a.F, bb_ = pb / a.F;
@@ -293,11 +215,13 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
       ra[i] = a.r[oa + nc];
       rb[i] = a.r[ob + nc];
     }
+    if constexpr (!MAG) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int k = lt + TPF * j, kc = k < KB ? k : 0;
-      ta[j] = a.tm[(size_t)pa * KB + kc];
-      tb[j] = a.tm[(size_t)pb * KB + kc];
+      for (int j = 0; j < NB; ++j) {
+        const int k = lt + TPF * j, kc = k < KB ? k : 0;
+        ta[j] = a.tm[(size_t)pa * KB + kc];
+        tb[j] = a.tm[(size_t)pb * KB + kc];
+      }
     }
   };
   if (blockIdx.x * FPI < npairs) load_pair(blockIdx.x * FPI);
@@ -307,80 +231,90 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int n = lt + i * TPF;
-      const bool in = n < a.win;
-      bA[n] = in ? f32x2{ra[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
-      bB[n] = in ? f32x2{rb[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
+      bA[n] = n < a.win ? f32x2{ra[i] * wn[n], rb[i] * wn[n]} : f32x2{0.f, 0.f};
     }
-    float mxa[NB], mxb[NB];
+    float mxa[MAG ? 1 : NB], mxb[MAG ? 1 : NB];
+    if constexpr (!MAG) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      mxa[j] = ta[j];
-      mxb[j] = tb[j];
+      for (int j = 0; j < NB; ++j) {
+        mxa[j] = ta[j];
+        mxb[j] = tb[j];
+      }
     }
     if (p0 + gridDim.x * FPI < npairs) load_pair(p0 + gridDim.x * FPI);  // lands during this pair's FFTs
     __syncthreads();
-    f32x2* Ra = fft<N, false, TPF>(bA, bC, tw, lt);
-    f32x2* sc = (Ra == bA) ? bC : bA;
-    f32x2* Rb = fft<N, false, TPF>(bB, sc, tw, lt);
-    // the buffer holding neither spectrum receives H
-    f32x2* H = (Ra != bA && Rb != bA) ? bA : ((Ra != bB && Rb != bB) ? bB : bC);
+    f32x2* Z = fft<N, false, TPF>(bA, bB, tw, lt);
+    f32x2* sc = (Z == bA) ? bB : bA;
     float sda = 0.f, sxa = 0.f, sdb = 0.f, sxb = 0.f;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int k = lt + TPF * j;
       if (k < KB) {
-        const f32x2 rka = Ra[k], rkb = Rb[k];
+        // bins k and N-k of Z are read and (GRAD) rewritten by this thread only: H is built in place
+        const int km = (N - k) & (N - 1);
+        const f32x2 zk = Z[k], zm = Z[km];
+        const f32x2 rka = f32x2{0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
+        const f32x2 rkb = f32x2{0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x)};
         const float mra = cabs2(rka), mrb = cabs2(rkb);
-        const float da = mxa[j] - mra, db = mxb[j] - mrb;
-        sda += da * da;
-        sxa += mxa[j] * mxa[j];
-        sdb += db * db;
-        sxb += mxb[j] * mxb[j];
-        if constexpr (GRAD) {
-          // dL/d(Re,Im)R_k = (|R|-|X|) R/|R| (0 at |R| = 0); H = H_a + i H_b, each the Hermitian extension
-          // of G/2 (G at k = 0, N/2)
-          const float ga = mra > 0.f ? (mra - mxa[j]) / mra : 0.f;
-          const float gb = mrb > 0.f ? (mrb - mxb[j]) / mrb : 0.f;
-          const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
-          if (k == 0 || k == N / 2) {
-            H[k] = f32x2{Ga.x, Gb.x};
-          } else {
-            H[k] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
-            H[N - k] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
+        if constexpr (MAG) {
+          if (acta) a.out[(size_t)fa * KB + k] = mra;
+          if (actb) a.out[(size_t)fb * KB + k] = mrb;
+        } else {
+          const float da = mxa[j] - mra, db = mxb[j] - mrb;
+          sda += da * da;
+          sxa += mxa[j] * mxa[j];
+          sdb += db * db;
+          sxb += mxb[j] * mxb[j];
+          if constexpr (GRAD) {
+            // dL/d(Re,Im)R_k = (|R|-|X|) R/|R| (0 at |R| = 0); H = H_a + i H_b, each the Hermitian extension
+            // of G/2 (G at k = 0, N/2)
+            const float ga = mra > 0.f ? (mra - mxa[j]) / mra : 0.f;
+            const float gb = mrb > 0.f ? (mrb - mxb[j]) / mrb : 0.f;
+            const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
+            if (k == 0 || k == N / 2) {
+              Z[k] = f32x2{Ga.x, Gb.x};
+            } else {
+              Z[k] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
+              Z[km] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
+            }
           }
         }
       }
     }
-    sda = warp_sum(sda);
-    sxa = warp_sum(sxa);
-    sdb = warp_sum(sdb);
-    sxb = warp_sum(sxb);
-    if ((tid & 63) == 0) {
-      red[0][wave] = sda;
-      red[1][wave] = sxa;
-      red[2][wave] = sdb;
-      red[3][wave] = sxb;
+    if constexpr (!MAG) {
+      sda = warp_sum(sda);
+      sxa = warp_sum(sxa);
+      sdb = warp_sum(sdb);
+      sxb = warp_sum(sxb);
+      if ((tid & 63) == 0) {
+        red[0][wave] = sda;
+        red[1][wave] = sxa;
+        red[2][wave] = sdb;
+        red[3][wave] = sxb;
+      }
     }
     __syncthreads();  // also orders the H writes before the inverse FFT
-    if (lt == 0) {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (!MAG) {
+      if (lt == 0) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int w = 0; w < WPF; ++w)
+        for (int w = 0; w < WPF; ++w)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) s[v] += red[v][sl * WPF + w];
-      if (acta) {
-        a.part[2 * (size_t)fa] = s[0];
-        a.part[2 * (size_t)fa + 1] = s[1];
-      }
-      if (actb) {
-        a.part[2 * (size_t)fb] = s[2];
-        a.part[2 * (size_t)fb + 1] = s[3];
+          for (int v = 0; v < 4; ++v) s[v] += red[v][sl * WPF + w];
+        if (acta) {
+          a.part[2 * (size_t)fa] = s[0];
+          a.part[2 * (size_t)fa + 1] = s[1];
+        }
+        if (actb) {
+          a.part[2 * (size_t)fb] = s[2];
+          a.part[2 * (size_t)fb + 1] = s[3];
+        }
       }
     }
     if constexpr (GRAD) {
-      const f32x2* Y = fft<N, true, TPF>(H, Ra, tw, lt);  // Ra's spectrum is no longer read
-      float* oa = a.fg + (size_t)fa * a.win;
-      float* ob = a.fg + (size_t)fb * a.win;
+      const f32x2* Y = fft<N, true, TPF>(Z, sc, tw, lt);
+      float* oa = a.out + (size_t)fa * a.win;
+      float* ob = a.out + (size_t)fb * a.win;
       for (int n = lt; n < a.win; n += TPF) {
         const f32x2 y = Y[n];
         if (acta) oa[n] = y.x * wn[n];
@@ -483,7 +417,7 @@ __global__ __launch_bounds__(256) void spec_gather_kernel(SpecGatherArgs a) {
   }
 }
 
-template <int N, int MODE>
+template <int N>
 static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
   constexpr int FPI = 256 / spec_tpf<N>();
   const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((fa.win + 3) & ~3) * sizeof(float) +
@@ -491,32 +425,31 @@ static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
   const int nframes = fa.B * fa.F;
   const int groups = (nframes + FPI - 1) / FPI;
   const int grid = groups < 2048 ? groups : 2048;
-  hipLaunchKernelGGL((spec_frame_kernel<N, MODE>), dim3(grid), dim3(256), lds, s, fa);
+  hipLaunchKernelGGL((spec_frame_kernel<N>), dim3(grid), dim3(256), lds, s, fa);
   VQA_LAUNCHED("spec_frame_kernel");
   return VQA_OK;
 }
 
 static bool spec_n_ok(int n) { return n == 256 || n == 512 || n == 1024 || n == 2048; }
 
-template <int MODE>
 static int dispatch_frames(int n_fft, const SpecFrameArgs& fa, hipStream_t s) {
   switch (n_fft) {
-    case 256: return launch_frames<256, MODE>(fa, s);
-    case 512: return launch_frames<512, MODE>(fa, s);
-    case 1024: return launch_frames<1024, MODE>(fa, s);
-    case 2048: return launch_frames<2048, MODE>(fa, s);
+    case 256: return launch_frames<256>(fa, s);
+    case 512: return launch_frames<512>(fa, s);
+    case 1024: return launch_frames<1024>(fa, s);
+    case 2048: return launch_frames<2048>(fa, s);
     default: set_error("spectral: n_fft %d unsupported (256, 512, 1024, 2048)", n_fft); return VQA_E_UNSUPPORTED;
   }
 }
 
-template <int N, bool GRAD>
+template <int N, int MODE>
 static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
   constexpr int FPI = 256 / spec_tpf<N>();
   const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((pa.win + 3) & ~3) * sizeof(float) +
-                     (size_t)FPI * 3 * N * sizeof(f32x2);
+                     (size_t)FPI * 2 * N * sizeof(f32x2);
   static size_t lds_set = 0;
   if (lds > 65536 && lds > lds_set) {
-    if (hipFuncSetAttribute((const void*)spec_pair_kernel<N, GRAD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)spec_pair_kernel<N, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess) {
       (void)hipGetLastError();
       set_error("spectral: cannot reserve %zu B of LDS", lds);
@@ -527,18 +460,18 @@ static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
   const int npairs = (pa.B * pa.F + 1) / 2;
   const int groups = (npairs + FPI - 1) / FPI;
   const int grid = groups < 2048 ? groups : 2048;
-  hipLaunchKernelGGL((spec_pair_kernel<N, GRAD>), dim3(grid), dim3(256), lds, s, pa);
+  hipLaunchKernelGGL((spec_pair_kernel<N, MODE>), dim3(grid), dim3(256), lds, s, pa);
   VQA_LAUNCHED("spec_pair_kernel");
   return VQA_OK;
 }
 
-template <bool GRAD>
+template <int MODE>
 static int dispatch_pairs(int n_fft, const SpecPairArgs& pa, hipStream_t s) {
   switch (n_fft) {
-    case 256: return launch_pairs<256, GRAD>(pa, s);
-    case 512: return launch_pairs<512, GRAD>(pa, s);
-    case 1024: return launch_pairs<1024, GRAD>(pa, s);
-    case 2048: return launch_pairs<2048, GRAD>(pa, s);
+    case 256: return launch_pairs<256, MODE>(pa, s);
+    case 512: return launch_pairs<512, MODE>(pa, s);
+    case 1024: return launch_pairs<1024, MODE>(pa, s);
+    case 2048: return launch_pairs<2048, MODE>(pa, s);
     default: set_error("spectral: n_fft %d unsupported (256, 512, 1024, 2048)", n_fft); return VQA_E_UNSUPPORTED;
   }
 }
@@ -596,9 +529,8 @@ static int spec_target(const float* x, float* tg, const SpecLayout& L, int B, in
   hipLaunchKernelGGL(spec_tables_kernel, dim3((maxn + 255) / 256, nres), dim3(256), 0, s, tb);
   VQA_LAUNCHED("spec_tables_kernel");
   for (int i = 0; i < nres; ++i) {
-    SpecFrameArgs fa{x, nullptr, nullptr, nullptr, tg + L.tm[i], tg + L.tw[i], tg + L.wn[i], B, T, L.F[i], hop[i],
-                     win[i]};
-    if (int rc = dispatch_frames<SPEC_MAG>(n_fft[i], fa, s)) return rc;
+    SpecPairArgs pa{x, nullptr, tg + L.tm[i], nullptr, tg + L.tw[i], tg + L.wn[i], B, T, L.F[i], hop[i], win[i]};
+    if (int rc = dispatch_pairs<PAIR_MAG>(n_fft[i], pa, s)) return rc;
   }
   return VQA_OK;
 }
@@ -612,7 +544,7 @@ static int spec_loss(const float* tg, const float* r, float* loss_out, float* dr
   for (int i = 0; i < nres; ++i) {
     SpecPairArgs pa{r, tg + L.tm[i], ws + L.fg[i], ws + L.part[i], tg + L.tw[i], tg + L.wn[i], B, T, L.F[i], hop[i],
                     win[i]};
-    const int rc = grad ? dispatch_pairs<true>(n_fft[i], pa, s) : dispatch_pairs<false>(n_fft[i], pa, s);
+    const int rc = grad ? dispatch_pairs<PAIR_GRAD>(n_fft[i], pa, s) : dispatch_pairs<PAIR_LOSS>(n_fft[i], pa, s);
     if (rc != VQA_OK) return rc;
     sa.part[i] = ws + L.part[i];
     sa.F[i] = L.F[i];
@@ -709,6 +641,6 @@ extern "C" int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int 
           "stft_magnitude: bad arguments (B=%d T=%d n_fft=%d hop=%d win=%d)", B, T, n_fft, hop, win);
   const int F = 1 + (T - win) / hop;
   // no workspace in this entry point: the kernel evaluates its twiddles and window itself
-  SpecFrameArgs fa{x, nullptr, nullptr, nullptr, mag, nullptr, nullptr, B, T, F, hop, win};
-  return dispatch_frames<SPEC_MAG>(n_fft, fa, (hipStream_t)stream);
+  SpecFrameArgs fa{x, mag, nullptr, nullptr, B, T, F, hop, win};
+  return dispatch_frames(n_fft, fa, (hipStream_t)stream);
 }
