@@ -427,7 +427,7 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   const bool pair = a.wmode == W_PAIR;
   const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
   const bool relu = a.flags & VQA_PRE_RELU;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int ko = M::koff(lane);
   constexpr int ESZ = (int)sizeof(T);
   const int erow = pair ? O / 2 : O;  // elements per output row (full resolution)
@@ -468,7 +468,9 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < a.K; ++k) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // K <= 4 (host-checked): unrolled, uniform exit
+      if (k >= a.K) break;
       const T* wk = wl + (size_t)k * O * WS + (lane & 15) * WS + ko;
       const T* xk = xl + (size_t)(k * a.D) * XS + ko;
 #pragma unroll
@@ -592,19 +594,23 @@ template <> __device__ __forceinline__ void store_out4<float>(__amdgpu_buffer_rs
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
 }
 
-template <class T, int PVX, int NEP, bool FW> constexpr int conv32_waves() {
+template <class T, int O, int PVX, int NEP, bool FW> constexpr int conv32_waves() {
   if (FW) return sizeof(T) == 2 ? 3 : 2;
-  return (PVX + NEP * (int)sizeof(T)) <= 7 ? 4 : ((PVX + NEP * (int)sizeof(T)) <= 11 ? 3 : 2);
+  const int regs = PVX + NEP * (int)sizeof(T) * (O / 32) + (O / 32 - 1) * 4;
+  return regs <= 7 ? 4 : (regs <= 11 ? 3 : 2);
 }
 
 // x-row byte offset that stays out of range after adding any tile base (|base| < 2^30)
 constexpr int kOOB = -0x40000000;
 
-template <class T, int PVX, int NEP, bool FW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv32_waves<T, PVX, NEP, FW>(), 8)))
+// O = 64 is the PAIR layout (conv-transpose forward, stride-2 data-gradient): output row j holds the two
+// full-resolution rows 2j, 2j+1 (32 channels each), i.e. the same bytes as the (B, 2T, 32) tensor.
+template <class T, int O, int PVX, int NEP, bool FW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv32_waves<T, O, PVX, NEP, FW>(), 8)))
 void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   typedef Mfma<T> M;
-  constexpr int C = 32, O = 32, TM = 128, NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
+  static_assert(O == 32 || (O == 64 && !FW), "conv32: O = 32, or the 64-wide PAIR layout without FW");
+  constexpr int C = 32, TM = 128, NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
   constexpr int ESZ = (int)sizeof(T), VEC = 16 / ESZ, CPR = C / VEC, ROWB = C * ESZ;
   constexpr int XS = C + lds_pad<T>(), WS = XS;
   constexpr int RSTEP = 256 / CPR;  // x rows between a thread's consecutive chunks
@@ -621,7 +627,7 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   if (tbeg >= tend) return;
   const bool do_mask = a.flags & VQA_POST_MASK, do_res = a.flags & VQA_ADD_RESIDUAL;
   const bool relu = a.flags & VQA_PRE_RELU;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int ko = M::koff(lane);
   const int rows_in = (TM - 1) * a.S + (a.K - 1) * a.D + 1;
   // epilogue tensor slots: [mask or conv input (FW)] then [residual]
@@ -630,7 +636,9 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   const void* ep1 = a.resid;
   const T* ml = (const T*)el;                                   // valid when has_m
   const T* rl = (const T*)(el + (has_m ? EBYTES : 0));          // valid when do_res
-  const unsigned xbytes = (unsigned)a.T_in * ROWB, obytes = (unsigned)a.T_out * O * ESZ;
+  const unsigned xbytes = (unsigned)a.T_in * ROWB;
+  // PAIR: the item's valid bytes end at full-resolution row T_full (the range check drops the rest)
+  const unsigned obytes = O == 64 ? (unsigned)a.T_full * (O / 2) * ESZ : (unsigned)a.T_out * O * ESZ;
 
   // per-thread chunk geometry, fixed for the launch
   const int q = threadIdx.x % CPR, row0 = threadIdx.x / CPR;
@@ -676,8 +684,8 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   f32x4 bias[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int o = mt * 16 + 4 * (lane >> 4);
-    bias[mt] = a.bias ? f32x4{a.bias[o], a.bias[o + 1], a.bias[o + 2], a.bias[o + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int o = mt * 16 + 4 * (lane >> 4), bo = O == 64 ? (o & 31) : o;  // PAIR: both halves share the bias
+    bias[mt] = a.bias ? f32x4{a.bias[bo], a.bias[bo + 1], a.bias[bo + 2], a.bias[bo + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
   stage_weights<T, C, O>(a, wl, WS);
@@ -693,7 +701,9 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < a.K; ++k) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // K <= 4 (host-checked): unrolled, uniform exit
+      if (k >= a.K) break;
       const T* wk = wl + (size_t)k * O * WS + (lane & 15) * WS + ko;
       const T* xk = xl + (size_t)(k * a.D) * XS + ko;
 #pragma unroll
@@ -1295,11 +1305,11 @@ static int launch_gather_mfma(const GatherArgs& a, hipStream_t s) {
 }
 
 // ---- the 32-channel kernel
-template <class T, int PVX, int NEP, bool FW>
+template <class T, int O, int PVX, int NEP, bool FW>
 static int launch_conv32_k(const GatherArgs& a, hipStream_t s, int* nwg_out) {
   constexpr int ESZ = (int)sizeof(T), XS = 32 + lds_pad<T>(), XROWS = 256 / (32 / (16 / ESZ)) * PVX;
-  const size_t lds = ((size_t)a.K * 32 * XS + (size_t)XROWS * XS) * ESZ + (size_t)NEP * 128 * 32 * ESZ;
-  const void* fn = (const void*)conv32_kernel<T, PVX, NEP, FW>;
+  const size_t lds = ((size_t)a.K * O * XS + (size_t)XROWS * XS) * ESZ + (size_t)NEP * 128 * O * ESZ;
+  const void* fn = (const void*)conv32_kernel<T, O, PVX, NEP, FW>;
   static size_t lds_set = 0;
   const int rc = ensure_dyn_lds(fn, lds, &lds_set, "conv32_kernel");
   if (rc != VQA_OK) return rc;
@@ -1310,7 +1320,7 @@ static int launch_conv32_k(const GatherArgs& a, hipStream_t s, int* nwg_out) {
   int tpw = 0;
   const int nwg = persistent_grid(fn, lds, &per_cu, &per_cu_lds, ntiles, &tpw);
   if (nwg_out) *nwg_out = nwg;
-  hipLaunchKernelGGL((conv32_kernel<T, PVX, NEP, FW>), dim3(nwg), dim3(256), lds, s, a, ntm, ntiles, tpw);
+  hipLaunchKernelGGL((conv32_kernel<T, O, PVX, NEP, FW>), dim3(nwg), dim3(256), lds, s, a, ntm, ntiles, tpw);
   VQA_LAUNCHED("conv32_kernel");
   return VQA_OK;
 }
@@ -1318,19 +1328,25 @@ static int launch_conv32_k(const GatherArgs& a, hipStream_t s, int* nwg_out) {
 template <class T, int PVX, bool FW>
 static int launch_conv32_n(const GatherArgs& a, int nep, hipStream_t s, int* nwg_out) {
   if constexpr (!FW) {
-    if (nep == 0) return launch_conv32_k<T, PVX, 0, FW>(a, s, nwg_out);
+    if (a.O == 64) {
+      if (nep == 0) return launch_conv32_k<T, 64, PVX, 0, false>(a, s, nwg_out);
+      if (nep == 1) return launch_conv32_k<T, 64, PVX, 1, false>(a, s, nwg_out);
+      return launch_conv32_k<T, 64, PVX, 2, false>(a, s, nwg_out);
+    }
+    if (nep == 0) return launch_conv32_k<T, 32, PVX, 0, FW>(a, s, nwg_out);
   }
-  if (nep == 1) return launch_conv32_k<T, PVX, 1, FW>(a, s, nwg_out);
-  return launch_conv32_k<T, PVX, 2, FW>(a, s, nwg_out);
+  if (nep == 1) return launch_conv32_k<T, 32, PVX, 1, FW>(a, s, nwg_out);
+  return launch_conv32_k<T, 32, PVX, 2, FW>(a, s, nwg_out);
 }
 
 // x chunks per thread the 32-channel kernel stages for this launch (0: not applicable)
 static int conv32_pvx(const GatherArgs& a, int dtype, bool fw) {
-  if (a.C != 32 || a.O != 32 || a.wmode == W_PAIR || a.K > 4 || a.S > 2) return 0;
+  const bool pair64 = a.O == 64 && a.wmode == W_PAIR && !fw && a.T_full <= 2 * a.T_out;
+  if (a.C != 32 || !((a.O == 32 && a.wmode != W_PAIR) || pair64) || a.K > 4 || a.S > 2) return 0;
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return 0;
   if (fw && (a.S != 1 || a.K > 3 || a.wmode != W_FLIP_T)) return 0;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
-  if ((long long)a.T_in * 32 * esz >= (1ll << 29) || (long long)a.T_out * 32 * esz >= (1ll << 29)) return 0;
+  if ((long long)a.T_in * 32 * esz >= (1ll << 29) || (long long)a.T_out * a.O * esz >= (1ll << 29)) return 0;
   const int rows_in = 127 * a.S + (a.K - 1) * a.D + 1;
   const int chunks = rows_in * 32 * esz / 16;
   const int pv = (chunks + 255) / 256;
@@ -1340,7 +1356,7 @@ static int conv32_pvx(const GatherArgs& a, int dtype, bool fw) {
   for (int i = 0; i < nopt; ++i) {
     if (pv <= opts[i]) {
       const int xs = 32 + 16 / esz, xrows = 256 / (32 * esz / 16) * opts[i];
-      const size_t lds = ((size_t)a.K * 32 * xs + (size_t)xrows * xs) * esz + 2 * 128 * 32 * esz;
+      const size_t lds = ((size_t)a.K * a.O * xs + (size_t)xrows * xs) * esz + 2 * 128 * (size_t)a.O * esz;
       return lds <= 150 * 1024 ? opts[i] : 0;
     }
   }
@@ -1362,6 +1378,7 @@ static int launch_conv32(const GatherArgs& a, int pvx, hipStream_t s, int* nwg_o
 
 static bool mfma_ok(const GatherArgs& a, int dtype) {
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return false;
+  if (a.K > 4) return false;  // the kernel's tap loop is unrolled for K <= 4
   if (!((a.C == 32 || a.C == 64) && (a.O == 32 || a.O == 64 || a.O == 128))) return false;
   const int tm = gather_tm(a.O, a.S);
   const int rows_in = (tm - 1) * a.S + (a.K - 1) * a.D + 1;
