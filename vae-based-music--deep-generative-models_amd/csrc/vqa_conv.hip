@@ -603,13 +603,13 @@ template <class T, int O, int PVX, int NEP, bool FW> constexpr int conv32_waves(
 // x-row byte offset that stays out of range after adding any tile base (|base| < 2^30)
 constexpr int kOOB = -0x40000000;
 
-// O = 64 is the PAIR layout (conv-transpose forward, stride-2 data-gradient): output row j holds the two
-// full-resolution rows 2j, 2j+1 (32 channels each), i.e. the same bytes as the (B, 2T, 32) tensor.
+// O = 64: a 32 -> 64 conv, or the PAIR layout (conv-transpose forward, stride-2 data-gradient) whose
+// output row j holds the two full-resolution rows 2j, 2j+1 (32 channels each) — the bytes of (B, 2T, 32).
 template <class T, int O, int PVX, int NEP, bool FW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv32_waves<T, O, PVX, NEP, FW>(), 8)))
 void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   typedef Mfma<T> M;
-  static_assert(O == 32 || (O == 64 && !FW), "conv32: O = 32, or the 64-wide PAIR layout without FW");
+  static_assert(O == 32 || (O == 64 && !FW), "conv32: O = 32 or 64 (64 without FW)");
   constexpr int C = 32, TM = 128, NW = 4, RW = TM / NW, NT = RW / 16, MT = O / 16;
   constexpr int ESZ = (int)sizeof(T), VEC = 16 / ESZ, CPR = C / VEC, ROWB = C * ESZ;
   constexpr int XS = C + lds_pad<T>(), WS = XS;
@@ -638,7 +638,8 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   const T* rl = (const T*)(el + (has_m ? EBYTES : 0));          // valid when do_res
   const unsigned xbytes = (unsigned)a.T_in * ROWB;
   // PAIR: the item's valid bytes end at full-resolution row T_full (the range check drops the rest)
-  const unsigned obytes = O == 64 ? (unsigned)a.T_full * (O / 2) * ESZ : (unsigned)a.T_out * O * ESZ;
+  const bool pair = a.wmode == W_PAIR;
+  const unsigned obytes = pair ? (unsigned)a.T_full * (O / 2) * ESZ : (unsigned)a.T_out * O * ESZ;
 
   // per-thread chunk geometry, fixed for the launch
   const int q = threadIdx.x % CPR, row0 = threadIdx.x / CPR;
@@ -684,7 +685,7 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   f32x4 bias[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int o = mt * 16 + 4 * (lane >> 4), bo = O == 64 ? (o & 31) : o;  // PAIR: both halves share the bias
+    const int o = mt * 16 + 4 * (lane >> 4), bo = pair ? (o & (O / 2 - 1)) : o;  // PAIR: halves share the bias
     bias[mt] = a.bias ? f32x4{a.bias[bo], a.bias[bo + 1], a.bias[bo + 2], a.bias[bo + 3]} : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
@@ -1341,8 +1342,8 @@ static int launch_conv32_n(const GatherArgs& a, int nep, hipStream_t s, int* nwg
 
 // x chunks per thread the 32-channel kernel stages for this launch (0: not applicable)
 static int conv32_pvx(const GatherArgs& a, int dtype, bool fw) {
-  const bool pair64 = a.O == 64 && a.wmode == W_PAIR && !fw && a.T_full <= 2 * a.T_out;
-  if (a.C != 32 || !((a.O == 32 && a.wmode != W_PAIR) || pair64) || a.K > 4 || a.S > 2) return 0;
+  const bool o64 = a.O == 64 && !fw && (a.wmode != W_PAIR || a.T_full <= 2 * a.T_out);
+  if (a.C != 32 || !((a.O == 32 && a.wmode != W_PAIR) || o64) || a.K > 4 || a.S > 2) return 0;
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return 0;
   if (fw && (a.S != 1 || a.K > 3 || a.wmode != W_FLIP_T)) return 0;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
