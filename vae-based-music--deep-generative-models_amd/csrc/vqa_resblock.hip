@@ -40,7 +40,8 @@ struct ResArgs {
   float* part_a;  // backward: [nwg][3*C*C + C] (dW_a | db_a)
   float* part_b;  // backward: [nwg][3*C*C + C] (dW_b | db_b)
   int B, T, d;
-  int ntm, ntiles, tpw;
+  int ntm, ntiles, tpw, textra;  // workgroup w owns tiles [w tpw + min(w, textra), +tpw + (w < textra))
+  int nwg;
   int skip;  // development ablation only (VQA_RESBLOCK_SKIP): bit p skips backward phase p (outputs wrong)
 };
 
@@ -315,7 +316,8 @@ void resblock_fwd_kernel(ResArgs a) {
   const int d = DT > 0 ? DT : a.d, XR = HR + 2 * d;
   T* H = X + XR * XS;  // local i <-> row t0 - 1 + i, relu(h)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
+  const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
+            tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
   typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()], wfb[3][2][rs_ncc<T>()];
   load_wfrags<T, kRsFwdKperm>(wfa, a.wa);
@@ -414,7 +416,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   T* Y = X + XR * XS;           // local m <-> row t0 - d - 1 + m (dy)
   T* H = Y + YR * XS;           // local i <-> row t0 - d + i: relu(h), then dh
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int tbeg = blockIdx.x * a.tpw, tend = min(a.ntiles, tbeg + a.tpw);
+  const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
+            tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
   stage_wimg<T, true>(waF, a.wa);
   stage_wimg<T, false>(waT, a.wa);
@@ -651,9 +654,11 @@ static int bwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? r
 static void plan(ResArgs& a, int per_cu, int rt) {
   a.ntm = (a.T + rt - 1) / rt;
   a.ntiles = a.ntm * a.B;
-  int nwg = rs_cus() * per_cu;
-  if (nwg > a.ntiles) nwg = a.ntiles;
-  a.tpw = (a.ntiles + nwg - 1) / nwg;
+  // every slot gets floor(ntiles / nwg) tiles and the first (ntiles mod nwg) one more: workgroups w and
+  // w + #CUs (dispatched to the same CU) never both hold an extra tile while extras <= #CUs
+  a.nwg = std::min(rs_cus() * per_cu, a.ntiles);
+  a.tpw = a.ntiles / a.nwg;
+  a.textra = a.ntiles - a.tpw * a.nwg;
 }
 
 }  // namespace vqa
@@ -674,13 +679,13 @@ extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba,
   VQA_REQUIRE(vqa_resblock_supported(C, dilation, dtype), VQA_E_UNSUPPORTED,
               "resblock_fwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
   VQA_ARG((long long)T * C * 4 < (1ll << 30), "resblock_fwd: item too long for 32-bit buffer offsets (T=%d)", T);
-  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0, 0};
+  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0, 0, 0, 0};
   plan(a, 3, fwd_rt_of(dilation));
   const int esz = dtype == VQA_BF16 ? 2 : 4;
   // one LDS reservation for every dilation (the largest plan)
   const size_t lds = std::max(fwd_lds(RMAXD, esz, RTM), fwd_lds(27, esz, rs_fwd_rt(27)));
   const hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((a.ntiles + a.tpw - 1) / a.tpw);
+  const dim3 grid(a.nwg);
   const void* fn = dtype == VQA_BF16 ? rs_pick<RsFwd<bf16>>(dilation) : rs_pick<RsFwd<float>>(dilation);
   if (int rc = set_lds(fn, lds)) return rc;
   void* args[] = {&a};
@@ -709,14 +714,14 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   const size_t need = vqa_resblock_bwd_workspace(B, T, C, dilation, dtype);
   VQA_ARG(workspace && ws_bytes >= need, "resblock_bwd: workspace %zu < %zu bytes", ws_bytes, need);
   const int E = 3 * RC * RC + RC;
-  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0};
+  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0, 0, 0};
   static const int dbg_skip = [] {
     const char* e = getenv("VQA_RESBLOCK_SKIP");
     return e ? atoi(e) : 0;
   }();
   a.skip = dbg_skip;
   plan(a, kResPerCU, bwd_rt_of(dilation));
-  const int nwg = (a.ntiles + a.tpw - 1) / a.tpw;
+  const int nwg = a.nwg;
   a.part_b = a.part_a + (size_t)nwg * E;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
   const size_t lds = bwd_lds(dilation, esz, bwd_rt_of(dilation));

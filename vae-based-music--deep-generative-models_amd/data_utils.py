@@ -52,10 +52,12 @@ class SpectralTarget:
         self._ws = {}
 
     def workspace(self, grad: bool) -> torch.Tensor:
-        if grad not in self._ws:
+        """Loss scratch, one per stream (levels on concurrent streams never share it)."""
+        key = (grad, torch.cuda.current_stream(self.x.device).cuda_stream if self.x.is_cuda else 0)
+        if key not in self._ws:
             n = V.spectral_loss_target_workspace(self.B, self.T, *STFT_ARGS, with_grad=grad)
-            self._ws[grad] = V.workspace(n, self.x.device)
-        return self._ws[grad]
+            self._ws[key] = V.workspace(n, self.x.device)
+        return self._ws[key]
 
 
 def multispectral_loss_and_grad(target: SpectralTarget, recon: torch.Tensor, loss_out=None, need_grad=True):

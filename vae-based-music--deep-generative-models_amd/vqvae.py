@@ -19,6 +19,7 @@ data-parallel exchange is ONE all_reduce (RCCL over xGMI) of [grads | EMA sums |
 """
 from __future__ import annotations
 
+import os
 from itertools import chain
 from typing import Dict, List, Optional
 
@@ -132,6 +133,9 @@ class VQVAE:
         self.optimizer: Optional[Adam] = None
         self.vqvaes = [_LevelModel(self, l) for l in range(levels)]
         self._graph = None
+        # run the levels' independent forward/backward chains on one stream each (VQA_LEVEL_STREAMS=0: serial)
+        self.concurrent_levels = os.environ.get("VQA_LEVEL_STREAMS", "1") != "0"
+        self._streams = None
 
     # ------------------------------------------------------------------ keras-like API
     def compile(self, optimizer=None, **kwargs):
@@ -171,27 +175,50 @@ class VQVAE:
     def _compute(self, x: torch.Tensor, training_grads: bool):
         """Forward (+ backward when training_grads) of every level; EMA sums into the bucket."""
         self._stats_region.zero_()
-        # weight-gradient partials of every layer are reduced in one launch per level
-        self.store.deferred = V.Deferred() if training_grads else None
         target = SpectralTarget(x)
-        B = x.shape[0]
+        main = torch.cuda.current_stream(self.device)
+        streams = self._level_streams()
         for l in range(self.levels):
-            enc, vq, dec = self.encoders[l], self.vqs[l], self.decoders[l]
-            z = enc.forward(x, save=training_grads)
-            n_loc = z.shape[0] * z.shape[1]
-            row_offset, n_global = vqa_dp.global_row_range(n_loc, self.process_group)
-            q, _ = vq.forward(z, training=True, row_offset=row_offset, n_global=n_global, save=training_grads)
-            r = dec.forward(q, save=training_grads)
-            _, dr_spec = multispectral_loss_and_grad(target, r, loss_out=self.loss_slots[l, 2:3],
-                                                     need_grad=training_grads)
-            dr = torch.empty_like(r)
-            V.mse_loss(x, r, dr_spec, dr, self.loss_slots[l, 0:1])
-            if training_grads:
-                dq = dec.backward(dr)
-                dz = vq.backward(dq, n_global=n_loc)
-                enc.backward(dz)
-                self.store.deferred.flush()
+            if streams is None:
+                self._level_step(x, l, target, training_grads)
+                continue
+            streams[l].wait_stream(main)
+            with torch.cuda.stream(streams[l]):
+                self._level_step(x, l, target, training_grads)
+        if streams is not None:
+            for s in streams:
+                main.wait_stream(s)
         self.store.deferred = None
+
+    def _level_streams(self):
+        """One HIP stream per level when `concurrent_levels`: the levels share nothing but the input and
+        its spectrograms, so their kernel chains overlap (level 2's long tail of small, latency-bound
+        launches fills the gaps of level 0's HBM-bound ones). Every buffer a level writes is its own (its
+        layers' gradient slices, its VQ stats and loss slots, workspaces from its stream's pool)."""
+        if not self.concurrent_levels or self.device.type != "cuda":
+            return None
+        if self._streams is None:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(self.levels)]
+        return self._streams
+
+    def _level_step(self, x, l, target, training_grads):
+        # this level's weight-gradient partials are reduced in one launch at its end
+        self.store.deferred = V.Deferred() if training_grads else None
+        enc, vq, dec = self.encoders[l], self.vqs[l], self.decoders[l]
+        z = enc.forward(x, save=training_grads)
+        n_loc = z.shape[0] * z.shape[1]
+        row_offset, n_global = vqa_dp.global_row_range(n_loc, self.process_group)
+        q, _ = vq.forward(z, training=True, row_offset=row_offset, n_global=n_global, save=training_grads)
+        r = dec.forward(q, save=training_grads)
+        _, dr_spec = multispectral_loss_and_grad(target, r, loss_out=self.loss_slots[l, 2:3],
+                                                 need_grad=training_grads)
+        dr = torch.empty_like(r)
+        V.mse_loss(x, r, dr_spec, dr, self.loss_slots[l, 0:1])
+        if training_grads:
+            dq = dec.backward(dr)
+            dz = vq.backward(dq, n_global=n_loc)
+            enc.backward(dz)
+            self.store.deferred.flush()
 
     def _update(self, apply_grads: bool):
         world = self._world()
