@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 --stats kernel_stats.csv: top kernels and the dominant kernel family's combined
 average (all conv32_kernel<bf16, ...> instantiations), for profiles/.
 
-    python tools/stats_summary.py KERNEL_STATS_CSV [BENCH_JSON] > profiles/rNN_summary.md
+    python tools/stats_summary.py KERNEL_STATS_CSV [BENCH_JSON [BENCH_JSON_DEFAULT]] > profiles/rNN_summary.md
 """
 import csv
 import json
@@ -25,7 +25,13 @@ print(f"\nDominant kernel resblock_bwd_kernel<bf16> ({len(fam)} instantiations):
 if len(sys.argv) > 2:
     b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
     r = b["roofline"]
-    print(f"\nbench.py line of the same run: {b['ms_per_step']} ms/step, {b['value'] / 1e6:.2f} M {b['unit']}; "
+    print(f"\nbench.py line of the same (levels serialised, VQA_LEVEL_STREAMS=0) run: {b['ms_per_step']} ms/step, {b['value'] / 1e6:.2f} M {b['unit']}; "
           f"roofline avg_launch_us {r['avg_launch_us']}, achieved {r['achieved']} GB/s "
           f"({100 * r['frac']:.1f} % of {r['peak']}), traffic {r['traffic']} B/launch vs algorithmic "
           f"{r['algorithmic_bytes_per_launch']} B/launch.")
+if len(sys.argv) > 3:
+    b = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
+    r = b["roofline"]
+    print(f"\nbench.py line with default settings (levels on concurrent streams), no profiler: "
+          f"{b['ms_per_step']} ms/step, {b['value'] / 1e6:.2f} M {b['unit']}; roofline avg_launch_us "
+          f"{r['avg_launch_us']} ({100 * r['frac']:.1f} % of {r['peak']} {r['unit']}).")

@@ -15,6 +15,23 @@ step = rows[a + 1:b + 1]
 wall = (int(step[-1]["End_Timestamp"]) - int(step[0]["Start_Timestamp"])) / 1e6
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step) / 1e6
 print(f"step {k}: {len(step)} dispatches, wall {wall:.3f} ms, kernel-busy {busy:.3f} ms")
+# concurrent streams: time with >= 1 kernel running, and the busy time of each queue / stream
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in step)
+union, cur_s, cur_e = 0, iv[0][0], iv[0][1]
+for s0, e0 in iv[1:]:
+    if s0 > cur_e:
+        union += cur_e - cur_s
+        cur_s, cur_e = s0, e0
+    else:
+        cur_e = max(cur_e, e0)
+union += cur_e - cur_s
+print(f"  GPU busy (>= 1 kernel) {union / 1e6:.3f} ms, idle {wall - union / 1e6:.3f} ms")
+for col in ("Stream_Id", "Queue_Id"):
+    if col in step[0]:
+        per = collections.defaultdict(float)
+        for r in step:
+            per[r[col]] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        print(f"  per {col}: " + ", ".join(f"{q}: {t:.3f} ms" for q, t in sorted(per.items())))
 by = collections.defaultdict(lambda: [0, 0.0])
 for r in step:
     n = r["Kernel_Name"]
