@@ -125,6 +125,25 @@ __device__ __forceinline__ void st8_buf(__amdgpu_buffer_rsrc_t r, int byte_off, 
   }
 }
 
+// the lane's 8 channels kept as raw activation bits (4 or 8 dwords) and widened when used
+template <class T> struct Raw8 {
+  uint4 v[sizeof(T) / 2];
+  __device__ __forceinline__ void load(const T* p) {
+#pragma unroll
+    for (int i = 0; i < (int)sizeof(T) / 2; ++i) v[i] = ((const uint4*)p)[i];
+  }
+  __device__ __forceinline__ void unpack(f32x4& lo, f32x4& hi) const {
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 b = __builtin_bit_cast(bf16x8, v[0]);
+      lo = f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+      hi = f32x4{(float)b[4], (float)b[5], (float)b[6], (float)b[7]};
+    } else {
+      lo = __builtin_bit_cast(f32x4, v[0]);
+      hi = __builtin_bit_cast(f32x4, v[1]);
+    }
+  }
+};
+
 // (value > 0) for the lane's 8 channels read from LDS (bf16: signed 16-bit compares on the raw bits, so
 // -0 counts as not positive)
 template <class T> __device__ __forceinline__ void pos8(const T* p, bool (&m)[8]);
@@ -342,6 +361,15 @@ void resblock_fwd_kernel(ResArgs a) {
     const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RT;
     // h rows t0-1 .. t0+RT+14 (conv_b reads t0-1 .. t0+RT); rows outside the item are conv_b's SAME zeros
     const bool interior = t0 - 1 >= 0 && t0 - 1 + HR <= a.T;  // uniform: no SAME-padding rows in h
+    // y rows of this lane: n-tiles wave, wave+4, ... of RT/16; their residual x rows are read from X now, so
+    // X is free for the next tile as soon as conv_a is done
+    int ry[NJ];
+    Raw8<T> xres[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      ry[j] = min(wave + 4 * j, NT - 1) * 16;
+      xres[j].load(X + (ry[j] + pn + 1 + d) * XS + oc);
+    }
     auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
     auto wb_frag = [&](int k, int mt, int sc) { return wfb[k][mt][sc]; };
     {
@@ -374,29 +402,25 @@ void resblock_fwd_kernel(ResArgs a) {
           st8_buf<T>(rs_rsrc((T*)a.h + (size_t)n * a.T * RC, ibytes), (r * RC + oc) * (int)sizeof(T), v[0], v[1]);
       }
     }
-    __syncthreads();
+    __syncthreads();  // H complete; every read of X for this tile is done
+    if (tile + 1 < tend) {
+      nx.template store<false>(X);
+      if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2));
+    }
     {
       const __amdgpu_buffer_rsrc_t yr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
-      int rb[NJ];
       f32x4 acc[NJ][2];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) rb[j] = min(wave + 4 * j, NT - 1) * 16;
-      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, rb, 1);
+      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (wave + 4 * j >= NT) continue;
-        const int tl = rb[j] + pn;
+        const int tl = ry[j] + pn;
         f32x4 x0, x1;
-        ld8(X + (tl + 1 + d) * XS + oc, x0, x1);
+        xres[j].unpack(x0, x1);
         st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + (acc[j][0] + bbv[0]), x1 + (acc[j][1] + bbv[1]));
       }
     }
-    if (tile + 1 < tend) {
-      __syncthreads();  // every read of X and H for this tile is done
-      nx.template store<false>(X);
-      if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2));
-      __syncthreads();
-    }
+    if (tile + 1 < tend) __syncthreads();  // every read of H done; the next tile's X is in LDS
   }
 }
 
