@@ -30,6 +30,8 @@ def _q(t, dt):
 CONV_CASES = [
     # (C_in, C_out, K, stride, dilation, B, T)
     (1, 32, 4, 2, 1, 2, 1024),     # first encoder down conv (generic path, fp32 waveform in)
+    (1, 32, 4, 2, 1, 1, 1537),     # ... ragged: last row block partial, SAME pad on both ends
+    (1, 64, 3, 1, 3, 2, 700),      # one-input-channel kernel with 64 outputs, dilated
     (32, 32, 4, 2, 1, 2, 1000),    # down conv, ragged length
     (32, 32, 4, 2, 1, 1, 513),     # odd length: SAME pads (1, 2)
     (64, 32, 4, 2, 1, 3, 512),     # level>=1 first down conv

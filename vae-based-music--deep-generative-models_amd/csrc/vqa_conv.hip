@@ -120,6 +120,15 @@ template <> __device__ __forceinline__ void ld8_<float>(const float* p, float* v
   }
 }
 
+template <class T> __device__ __forceinline__ void st8_(T* p, const float* v);
+template <> __device__ __forceinline__ void st8_<bf16>(bf16* p, const float* v) {
+  *(bf16x8*)p = bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+}
+template <> __device__ __forceinline__ void st8_<float>(float* p, const float* v) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
 template <class TX, class TY, int OV>
 __global__ __launch_bounds__(256) void gather_thin_kernel(GatherArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -172,6 +181,25 @@ __global__ __launch_bounds__(256) void gather_thin_kernel(GatherArgs a) {
     const long long oi = out_index(a, n, t, o0);
     if (oi < 0) continue;
     const int bo = bias_index(a, o0);
+    if constexpr (OV == 8) {
+      if (a.O % 16 == 0) {  // the 8 channels are contiguous and 16-byte aligned in every mode: one vector access
+        float v[8], m[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = a.bias ? acc[q] + a.bias[bo + q] : acc[q];
+        if (a.flags & VQA_POST_MASK) {
+          ld8_((const TY*)a.mask + oi, m);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = m[q] > 0.f ? v[q] : 0.f;
+        }
+        if (a.flags & VQA_ADD_RESIDUAL) {
+          ld8_((const TY*)a.resid + oi, m);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = m[q] + v[q];
+        }
+        st8_((TY*)a.y + oi, v);
+        continue;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < OV; ++q) {
       float v = acc[q];
@@ -952,7 +980,7 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* v)
 
 template <class TX, class TG, bool WIDE_X>
 __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
-  constexpr int KM = 4, NM = 2;  // max taps, max narrow width
+  constexpr int KM = 4, NM = 2, U = 4;  // max taps, max narrow width, rows in flight per thread
   const int W = WIDE_X ? a.C : a.O;
   const int NN = WIDE_X ? a.O : a.C;
   const int VL = W / 8, RL = 256 / VL;
@@ -973,12 +1001,12 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
   if (rl < RL) {
-    // two rows per iteration, all loads issued before the FMAs (memory-level parallelism)
-    for (int t = tbeg + rl; t < tend; t += 2 * RL) {
-      float gv[2][WIDE_X ? NM : 8];
-      float xv[2][KM][WIDE_X ? 8 : NM];
+    // U rows per iteration, all loads issued before the FMAs (memory-level parallelism)
+    for (int t = tbeg + rl; t < tend; t += U * RL) {
+      float gv[U][WIDE_X ? NM : 8];
+      float xv[U][KM][WIDE_X ? 8 : NM];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int tt = t + u * RL;
         const bool okr = tt < tend;
         if (WIDE_X) {
@@ -1006,7 +1034,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         if (WIDE_X) {
           if (v == 0)
 #pragma unroll
@@ -1435,6 +1463,71 @@ static int launch_gather_thin(const GatherArgs& a, hipStream_t s) {
   return VQA_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// One-input-channel conv (the encoder's first conv on the waveform, encdec.py:33 with C = 1): a workgroup
+// owns CI1_RB output rows of one item; their input span is staged once in LDS (fp32), each lane holds the
+// K x 8 weights of its 8 output channels in registers and writes its rows' 8 channels as one 16-byte
+// (bf16) store — consecutive lanes write consecutive bytes. Per-row tap order k = 0..K-1 (as the gather
+// kernels).
+constexpr int CI1_RB = 512, CI1_KMAX = 8;
+
+template <class TX, class TY, int O>
+__global__ __launch_bounds__(256) void gather_ci1_kernel(GatherArgs a) {
+  constexpr int L = O / 8, RPP = 256 / L;  // lanes per row, rows per pass
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* xl = (float*)smem;
+  const int n = blockIdx.y, t0 = blockIdx.x * CI1_RB;
+  const int span = (CI1_RB - 1) * a.S + (a.K - 1) * a.D + 1, i0 = t0 * a.S - a.P;
+  const TX* X = (const TX*)a.x + (size_t)n * a.T_in;
+  const bool relu = a.flags & VQA_PRE_RELU;
+  for (int e = threadIdx.x; e < span; e += 256) {
+    const int ti = i0 + e;
+    float v = (ti >= 0 && ti < a.T_in) ? ld(X + ti) : 0.f;
+    xl[e] = relu ? fmaxf(v, 0.f) : v;
+  }
+  const int o8 = (threadIdx.x % L) * 8, rl = threadIdx.x / L;
+  float w[CI1_KMAX][8], b[8];
+#pragma unroll
+  for (int k = 0; k < CI1_KMAX; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[k][j] = k < a.K ? a.w[k * O + o8 + j] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = a.bias ? a.bias[o8 + j] : 0.f;
+  __syncthreads();
+  TY* Y = (TY*)a.y + (size_t)n * a.T_out * O;
+  for (int r = rl; r < CI1_RB && t0 + r < a.T_out; r += RPP) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < CI1_KMAX; ++k) {
+      if (k >= a.K) break;
+      const float xv = xl[r * a.S + k * a.D];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += xv * w[k][j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = acc[j] + b[j];
+    st8_(Y + (size_t)(t0 + r) * O + o8, acc);
+  }
+}
+
+template <class TX, class TY>
+static int launch_gather_ci1(const GatherArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)((CI1_RB - 1) * a.S + (a.K - 1) * a.D + 1) * sizeof(float);
+  const dim3 grid((a.T_out + CI1_RB - 1) / CI1_RB, a.B);
+  if (a.O == 32) hipLaunchKernelGGL((gather_ci1_kernel<TX, TY, 32>), grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL((gather_ci1_kernel<TX, TY, 64>), grid, dim3(256), lds, s, a);
+  VQA_LAUNCHED("gather_ci1_kernel");
+  return VQA_OK;
+}
+
+static bool ci1_ok(const GatherArgs& a) {
+  return a.C == 1 && a.wmode == W_DIRECT && (a.O == 32 || a.O == 64) && a.K <= CI1_KMAX &&
+         !(a.flags & (VQA_POST_MASK | VQA_ADD_RESIDUAL)) &&
+         (size_t)((CI1_RB - 1) * a.S + (a.K - 1) * a.D + 1) * sizeof(float) <= 64 * 1024;
+}
+
 int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);
   VQA_ARG(a.x && a.w && a.y, "null tensor pointer");
@@ -1449,6 +1542,12 @@ int run_gather(const GatherArgs& a, int dtype, hipStream_t s) {
   if (mfma_ok(a, dtype)) return dtype == VQA_BF16 ? launch_gather_mfma<bf16>(a, s) : launch_gather_mfma<float>(a, s);
   const bool xf = dtype == VQA_F32 || (a.flags & VQA_X_F32);
   const bool yf = dtype == VQA_F32 || (a.flags & VQA_Y_F32);
+  if (ci1_ok(a)) {
+    if (xf && yf) return launch_gather_ci1<float, float>(a, s);
+    if (xf) return launch_gather_ci1<float, bf16>(a, s);
+    if (yf) return launch_gather_ci1<bf16, float>(a, s);
+    return launch_gather_ci1<bf16, bf16>(a, s);
+  }
   if (a.O <= 8 && (a.C == 32 || a.C == 64) && a.wmode != W_PAIR && a.K <= 4 && a.S <= 2 && a.D <= 64) {
     if (xf && yf) return launch_gather_thinO<float, float>(a, s);
     if (xf) return launch_gather_thinO<float, bf16>(a, s);
@@ -1505,9 +1604,9 @@ static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O,
     const int rows_in = (p.TT - 1) * S + (K - 1) * D + 1;
     p.lds = ((size_t)p.TT * O + (size_t)rows_in * C) * 4;
   }
-  // ~512 workgroups (two per CU) for the MFMA kinds: each streams its rows once and partials stay
-  // small; the thin kinds have tiny partials and short per-row work, so they take 2048.
-  const long long target = (p.kind == WG_THIN_X || p.kind == WG_THIN_G) ? 2048 : 512;
+  // ~512 workgroups (two per CU): each streams its rows once (4 rows in flight per thread in the thin
+  // kinds) and the partials stay small
+  const long long target = 512;
   const long long per_item = (target + B - 1) / B;
   int ch = (int)((T_out + per_item - 1) / per_item);
   ch = ((ch + p.TT - 1) / p.TT) * p.TT;
