@@ -136,10 +136,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VQA_DIST_BACKEND=gloo + ranks sharing one GPU (local rank wrapped onto the visible devices) rehearses the
+    # DP path (split graphs around the exchange) on a one-GPU box; the driver's N>1 runs use RCCL ("nccl")
+    backend = os.environ.get("VQA_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     import vqa_lib as V
     from data_utils import synthetic_batch
     from vqvae import VQVAE
