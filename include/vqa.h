@@ -206,6 +206,13 @@ size_t vqa_mse_loss_workspace(int64_t n);
  * w -= alpha*m/(sqrt(v)+eps), with s = grad_scale. Does not touch *step. */
 int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, const int64_t* step, float lr,
                    float beta1, float beta2, float eps, float grad_scale, vqa_stream_t stream);
+/* The train step's metric trackers in one launch (replaces update_metrics, vqvae.py:262-304, and the VQ
+ * trackers, VectorQuantizer.py:149-159): macc is (4 + 7*levels) x (total, count) — rows loss, recon_loss,
+ * vqvae_loss, spectral_loss, then per level level/recon/vq/spectral loss, batch usage, usage, entropy;
+ * loss_slots (levels x 3: recon, commit, spectral) are scaled by `scale` (1/world) first; vq_metrics is
+ * levels x 3 (vqa_vq_ema_apply's metrics). Each row gets total += value, count += 1 (keras Mean). */
+int vqa_step_metrics(const float* loss_slots, const float* vq_metrics, float* macc, int levels, float scale,
+                     vqa_stream_t stream);
 /* *counter += delta on the stream (graph-capturable step counters). */
 int vqa_counter_add(int64_t* counter, int64_t delta, vqa_stream_t stream);
 

@@ -1,0 +1,74 @@
+"""One rank of the product data-parallel test (tests/test_gpu_dp.py; not collected by pytest).
+
+Runs VQVAE.train_step with a torch.distributed process group (gloo, every rank on cuda:0) on its shard of
+the global batch — eager, or as the two captured hipGraphs around the eager all_reduce — then one
+`vqvaes[0](x, training=True)` forward (the EMA on global statistics), and saves the resulting state.
+    python tests/dp_worker.py MODE OUT   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"), ROOT]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CFG = dict(input_len=4096, levels=1, latent_dim=64, down_depth=[3], strides=[2], num_embeddings=256,
+           residual_width=32, residual_depth=4, dilation_factor=3)
+B_LOCAL = 2
+
+
+def build(B, process_group=None):
+    from oracle import vqvae_ref as R
+    from vqvae import VQVAE
+    cfg = R.RefConfig(**CFG)
+    m = VQVAE((cfg.input_len, 1), cfg.levels, cfg.latent_dim, cfg.down_depth, cfg.strides,
+              num_embeddings=cfg.num_embeddings, residual_width=cfg.residual_width,
+              residual_depth=cfg.residual_depth, dilation_factor=cfg.dilation_factor, dtype="fp32",
+              device="cuda:0", process_group=process_group)
+    m.set_weights(R.init_params(cfg, 1))
+    m.set_vq_state(R.init_vq_state(cfg, 2))
+    m.compile()
+    return m
+
+
+def batches(world):
+    from oracle import vqvae_ref as R
+    return [R.synthetic_batch(B_LOCAL * world, CFG["input_len"], seed=90 + i) for i in range(3)]
+
+
+def snapshot(m):
+    P = m.layout["grads"][1]
+    return {"weights": m.store.flat.detach().cpu().clone(), "adam_m": m.optimizer.m.cpu().clone(),
+            "adam_v": m.optimizer.v.cpu().clone(), "stats": m.bucket[P:].detach().cpu().clone(),
+            "vq": [{k: torch.as_tensor(v) for k, v in st.items() if k != "calls"} | {"calls": st["calls"]}
+                   for st in m.get_vq_state()],
+            "results": {k: float(v) for k, v in m.results().items()}}
+
+
+def main():
+    mode, out = sys.argv[1], sys.argv[2]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = build(B_LOCAL)
+    xs = [x[rank * B_LOCAL:(rank + 1) * B_LOCAL] for x in batches(world)]
+    if mode == "eager":
+        m.train_step(xs[0])
+        m.train_step(xs[1])
+    else:  # one eager warm-up step on xs[0], then the captured step replayed on xs[1]
+        m.capture_train_step(xs[0], warmup=1)
+        m.train_step(xs[1])
+    torch.cuda.synchronize()
+    res = {"steps": snapshot(m)}
+    m.vqvaes[0](xs[2], training=True)  # forward-only EMA: global statistics under DP
+    torch.cuda.synchronize()
+    res["forward"] = snapshot(m)
+    torch.save(res, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

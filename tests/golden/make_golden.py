@@ -22,6 +22,12 @@ CFG1 = dict(input_len=4096, levels=1, latent_dim=64, down_depth=[3], strides=[2]
             residual_width=32, residual_depth=4, dilation_factor=3)
 
 
+def _rel_margin(dist):
+    """(second-smallest - smallest) / |smallest| of each row's fp64 distances: how far the row is from a tie."""
+    top2 = torch.topk(dist, 2, dim=1, largest=False).values
+    return ((top2[:, 1] - top2[:, 0]) / top2[:, 0].abs().clamp(min=1e-30)).numpy()
+
+
 def run(cfgd, B, steps, seed_x):
     cfg = R.RefConfig(**cfgd)
     params, vq = R.init_params(cfg, 1), R.init_vq_state(cfg, 2)
@@ -33,6 +39,7 @@ def run(cfgd, B, steps, seed_x):
         out["metrics"].append(m.train_step(x))
         out["grads"].append({n: g.numpy().astype(np.float64) for n, g in m.last["grads"].items()})
         out["idx"].append([i["idx"].numpy() for i in m.last["infos"]])
+        out.setdefault("margin", []).append([_rel_margin(i["dist"]) for i in m.last["infos"]])
     w, vqs = m.state_numpy()
     return cfg, params, vq, out, w, vqs
 
@@ -44,6 +51,7 @@ def main():
         arrs[f"x{s}"] = x
         for l, idx in enumerate(out["idx"][s]):
             arrs[f"idx{s}_l{l}"] = idx
+            arrs[f"margin{s}_l{l}"] = out["margin"][s][l]
         for n, g in out["grads"][s].items():
             arrs[f"grad{s}/{n}"] = g
     for n, v in params.items():

@@ -203,3 +203,108 @@ def test_vector_quantizer_layer_call(cuda):
     assert q.shape == x.shape and idx.shape == (3200,)
     assert torch.isfinite(vq.embeddings).all()
     assert float(vq.N_t.sum()) > 0
+
+
+def _fixed_order_sums(z, idx, K, tile=64):
+    """numpy float32 restatement of the deterministic EMA-sum order of vqa_vq_quantize (vqa_vq.hip): rows
+    sorted by (code, row); a code's sum is sequential over its rows inside each 64-position tile of the sorted
+    order; the tile partials of a code spanning tiles are summed sequentially in four contiguous quarters of its
+    tile range (the first tile's partial leads quarter 0), then ((q0 + q1) + q2) + q3."""
+    z = np.asarray(z, np.float32)
+    order = np.argsort(idx, kind="stable")
+    counts = np.bincount(idx, minlength=K)
+    seg = np.concatenate([[0], np.cumsum(counts)])
+    zs = z[order]
+    out = np.zeros((K, z.shape[1]), np.float32)
+
+    def seqsum(a):
+        return np.cumsum(a, axis=0, dtype=np.float32)[-1]
+    for k in range(K):
+        S, E = int(seg[k]), int(seg[k + 1])
+        if E <= S:
+            continue
+        ta, tb = S // tile, (E - 1) // tile
+        if ta == tb:
+            out[k] = seqsum(zs[S:E])
+            continue
+        parts = [seqsum(zs[S:(ta + 1) * tile])] + [seqsum(zs[t * tile:min(E, (t + 1) * tile)])
+                                                   for t in range(ta + 1, tb + 1)]
+        n = tb - ta
+        per = (n + 3) // 4
+        q = []
+        for v in range(4):
+            i0, i1 = min(n, v * per), min(n, (v + 1) * per)
+            s = parts[0] if v == 0 else np.zeros(z.shape[1], np.float32)
+            for t in range(i0, i1):
+                s = (s + parts[1 + t]).astype(np.float32)
+            q.append(s)
+        out[k] = ((q[0] + q[1]) + q[2]) + q[3]
+    return out, counts.astype(np.float32)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,D,K,crowd", [(20000, 64, 256, 0.0), (50000, 64, 2048, 0.7), (777, 8, 1024, 0.0),
+                                         (3001, 4, 16, 0.5), (262144, 64, 2048, 0.3)])
+def test_ema_sums_deterministic_fixed_order(cuda, dt, N, D, K, crowd):
+    """EMA sums (VectorQuantizer.py:123-124) are deterministic: bit-identical to the numpy float32 restatement
+    of their fixed summation order, bit-identical on a repeated call, counts exact; and within fp32 rounding
+    of the fp64 one-hot GEMM. `crowd`: fraction of rows sent to one code (a segment spanning many tiles)."""
+    g = torch.Generator().manual_seed(N + D + K)
+    z = torch.randn(N, D, generator=g).to(dt)
+    idx = torch.randint(0, K, (N,), generator=g)
+    if crowd:
+        idx[torch.rand(N, generator=g) < crowd] = 3
+    zd, idxd = z.cuda(), idx.cuda()
+    ETd = torch.randn(K, D, device=cuda)
+    outs = []
+    for _ in range(2):
+        q = torch.empty_like(zd)
+        commit = torch.zeros(1, device=cuda)
+        m_sumT = torch.zeros(K, D, device=cuda)
+        n_sum = torch.zeros(K, device=cuda)
+        V.vq_quantize(zd, ETd, idxd, q, commit, m_sumT, n_sum, 0.25)
+        outs.append((m_sumT.cpu().numpy(), n_sum.cpu().numpy(), float(commit)))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+    want, cnt = _fixed_order_sums(z.float().numpy(), idx.numpy(), K)
+    assert np.array_equal(outs[0][1], cnt)
+    assert np.array_equal(outs[0][0], want), f"max diff {np.abs(outs[0][0] - want).max()}"
+    ref = np.zeros((K, D))
+    np.add.at(ref, idx.numpy(), z.double().numpy())
+    scale = np.abs(z.double().numpy()).max() * np.sqrt(cnt.max())
+    assert np.abs(outs[0][0] - ref).max() <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("path", ["fp32", "bf16_direct", "bf16_split"])
+def test_argmin_nonfinite_rows_index_zero(cuda, path):
+    """A row whose distances are all NaN / +inf resolves to code 0 (tf.argmin's initial index) instead of an
+    out-of-range sentinel, and the quantizer's gathers stay in bounds."""
+    D, K, N = 64, 2048, 300
+    g = torch.Generator().manual_seed(1)
+    dt = torch.float32 if path == "fp32" else torch.bfloat16
+    z = torch.randn(N, D, generator=g)
+    z[5] = float("nan")
+    z[17, 3] = float("inf")
+    z[18, :] = float("-inf")
+    z = z.to(dt)
+    E = (torch.rand(D, K, generator=g) - 0.5) * 0.1
+    zd, Ed = z.cuda(), E.cuda()
+    esq = torch.empty(K, device=cuda)
+    V.vq_sqnorm(Ed, esq)
+    idx = torch.empty(N, dtype=torch.int64, device=cuda)
+    if path == "bf16_split":
+        E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=cuda)
+        V.vq_split_bf16x3(Ed, E3)
+        V.vq_argmin_split(zd, E3, esq, idx)  # N small: the codebook is split across workgroups
+    else:
+        V.vq_argmin(zd, Ed, esq, idx)
+    got = idx.cpu()
+    assert int(got[5]) == 0 and int(got[17]) == 0 and int(got[18]) == 0
+    assert bool(((got >= 0) & (got < K)).all())
+    q = torch.empty_like(zd)
+    commit = torch.zeros(1, device=cuda)
+    m_sumT = torch.zeros(K, D, device=cuda)
+    n_sum = torch.zeros(K, device=cuda)
+    V.vq_quantize(zd, Ed.t().contiguous(), idx, q, commit, m_sumT, n_sum, 0.25)
+    torch.cuda.synchronize()
+    assert float(n_sum.sum()) == N

@@ -91,3 +91,22 @@ def test_binding_fails_loudly_without_library(monkeypatch):
     monkeypatch.setattr(V, "_lib", None)
     with pytest.raises(ImportError, match="no CPU fallback"):
         V.lib()
+
+
+def test_keras_mean_trackers_monitor_loop():
+    """vqa_metrics.Mean / SlotMean have the keras tracker surface the reference's monitor uses
+    (src/callback/vae_monitor.py:64-65 reset loop, :70-72 name / result)."""
+    from vqa_metrics import Mean, SlotMean
+    acc = torch.zeros(3, 2)
+    ts = [SlotMean(f"m{i}", acc, i) for i in range(3)]
+    for i, t in enumerate(ts):
+        t.update_state(torch.tensor(float(i + 1)))
+        t.update_state(torch.tensor(float(3 * (i + 1))))
+    assert [float(t.result()) for t in ts] == [2.0, 4.0, 6.0]
+    for t in ts[:2]:
+        t.reset_state()
+    assert [float(t.result()) for t in ts] == [0.0, 0.0, 6.0] and float(acc[2, 1]) == 2.0
+    m = Mean("x", "cpu")
+    m.update_state(torch.tensor(5.0))
+    m.reset_states()
+    assert float(m.result()) == 0.0 and m.name == "x"

@@ -1,5 +1,8 @@
 #!/bin/bash
 # Phase ablation of the fused residual-block backward (GPU dev tool): time it with each phase skipped.
+# Builds an ablation libvqa (make ABLATION=1) and restores the product build at the end.
+make -C vae-based-music--deep-generative-models_amd/csrc clean >/dev/null && make -C vae-based-music--deep-generative-models_amd/csrc ABLATION=1 -j8 >/dev/null || exit 1
 for s in 0 1 2 4 8 16 31; do
   echo "skip=$s $(VQA_RESBLOCK_SKIP=$s timeout -k 10 120 python tools/resblock_sweep.py --T 32768 --reps 10 2>/dev/null | grep 'd= 9')"
 done
+make -C vae-based-music--deep-generative-models_amd/csrc clean >/dev/null && make -C vae-based-music--deep-generative-models_amd/csrc -j8 >/dev/null

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 import vqa_lib as V
-from vqa_metrics import Mean
+from vqa_metrics import Mean, SlotMean
 
 
 class VectorQuantizer:
@@ -64,6 +64,14 @@ class VectorQuantizer:
     @property
     def metrics(self):
         return [self.batch_usage_tracker, self.usage_tracker, self.entropy_tracker]
+
+    def bind_metrics(self, vq_metrics: torch.Tensor, macc: torch.Tensor, rows):
+        """Inside a VQVAE: the per-step usage / entropy values live in the model's (levels, 3) buffer and the
+        trackers are rows of its accumulator (updated by the model's one-launch vqa_step_metrics)."""
+        self.vq_metrics = vq_metrics
+        names = [m.name for m in self.metrics]
+        self.batch_usage_tracker, self.usage_tracker, self.entropy_tracker = (
+            SlotMean(n, macc, r) for n, r in zip(names, rows))
 
     # ---- statistics buffers (m_sumT (K, D) | n_sum (K) | RT (K, D)) ----
     def stats_size(self) -> int:

@@ -42,7 +42,7 @@ struct ResArgs {
   int B, T, d;
   int ntm, ntiles, tpw, textra;  // workgroup w owns tiles [w tpw + min(w, textra), +tpw + (w < textra))
   int nwg;
-  int skip;  // development ablation only (VQA_RESBLOCK_SKIP): bit p skips backward phase p (outputs wrong)
+  int skip;  // 0 in the product; -DVQA_RESBLOCK_ABLATION builds read VQA_RESBLOCK_SKIP (bit p skips phase p)
 };
 
 template <class T> constexpr int rs_stride() { return RC + lds_pad<T>(); }
@@ -739,11 +739,14 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   VQA_ARG(workspace && ws_bytes >= need, "resblock_bwd: workspace %zu < %zu bytes", ws_bytes, need);
   const int E = 3 * RC * RC + RC;
   ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0, 0, 0};
+#ifdef VQA_RESBLOCK_ABLATION
+  // development builds only (make ABLATION=1, tools/ablate_res.sh): phases skipped, gradients WRONG
   static const int dbg_skip = [] {
     const char* e = getenv("VQA_RESBLOCK_SKIP");
     return e ? atoi(e) : 0;
   }();
   a.skip = dbg_skip;
+#endif
   plan(a, kResPerCU, bwd_rt_of(dilation));
   const int nwg = a.nwg;
   a.part_b = a.part_a + (size_t)nwg * E;

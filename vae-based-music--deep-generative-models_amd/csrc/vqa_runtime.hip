@@ -66,6 +66,36 @@ __global__ void counter_add_kernel(int64_t* c, int64_t delta) {
   if (threadIdx.x == 0 && blockIdx.x == 0) c[0] += delta;
 }
 
+// The step's metric trackers (vqvae.py:262-304 update_metrics, VectorQuantizer.py:149-159) as one launch:
+// macc rows [loss, recon, vqvae, spectral] then per level [level, recon, vq, spectral, batch_usage, usage,
+// entropy], each (total, count). loss_slots = per level (recon, commit, spectral) sums over ranks, scaled by
+// 1/world; the Python sums of the reference are left folds: level = (recon + commit) + spectral,
+// total = ((0 + level_0) + level_1) + ...
+__global__ void step_metrics_kernel(const float* loss_slots, const float* vqm, float* macc, int levels,
+                                    float scale) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float tot = 0.f, tr = 0.f, tc = 0.f, ts = 0.f;
+  for (int l = 0; l < levels; ++l) {
+    const float r = loss_slots[3 * l] * scale, c = loss_slots[3 * l + 1] * scale, sp = loss_slots[3 * l + 2] * scale;
+    const float lv = (r + c) + sp;
+    tot += lv;
+    tr += r;
+    tc += c;
+    ts += sp;
+    const float v[7] = {lv, r, c, sp, vqm[3 * l], vqm[3 * l + 1], vqm[3 * l + 2]};
+    float* row = macc + 2 * (4 + 7 * l);
+    for (int i = 0; i < 7; ++i) {
+      row[2 * i] += v[i];
+      row[2 * i + 1] += 1.f;
+    }
+  }
+  const float g[4] = {tot, tr, tc, ts};
+  for (int i = 0; i < 4; ++i) {
+    macc[2 * i] += g[i];
+    macc[2 * i + 1] += 1.f;
+  }
+}
+
 static int blocks_for(long long n, int cap) {
   long long b = (n + 255) / 256;
   if (b > cap) b = cap;
@@ -111,5 +141,14 @@ extern "C" int vqa_counter_add(int64_t* counter, int64_t delta, vqa_stream_t str
   VQA_ARG(counter, "counter_add: null pointer");
   hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, delta);
   VQA_LAUNCHED("counter_add_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_step_metrics(const float* loss_slots, const float* vq_metrics, float* macc, int levels, float scale,
+                                vqa_stream_t stream) {
+  VQA_ARG(loss_slots && vq_metrics && macc && levels > 0, "step_metrics: bad arguments");
+  hipLaunchKernelGGL(step_metrics_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, loss_slots, vq_metrics, macc,
+                     levels, scale);
+  VQA_LAUNCHED("step_metrics_kernel");
   return VQA_OK;
 }

@@ -4,8 +4,8 @@
 //   get_code_indices :170-186  -> vq_argmin_mfma_kernel (fp32 MFMA distance tiles + wave argmin);
 //                                 no N x K distance matrix is materialised.
 //   one_hot @ E^T    :86-90    -> a row gather from ET = E^T (K, D) kept by the EMA kernel.
-//   commit loss      :97-99, straight-through :114 -> vq_quantize_kernel; EMA sums :123-124 ->
-//                                 vq_ema_sums_kernel (per-chunk LDS tables + a fixed-order reduction).
+//   commit loss      :97-99, straight-through :114 -> vq_quantize_kernel; EMA sums :123-124 -> a counting
+//                                 sort by code + fixed-order segment sums (deterministic, no float atomics).
 //   EMA + dead-code reset :126-145, metrics :149-159 -> vq_ema_apply_kernel / vq_metrics_kernel.
 // The reset candidates (tf.random.shuffle, :137) use an injected, seeded Feistel permutation.
 #include "vqa_common.h"
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const f
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       best[rt][r] = __builtin_inff();
-      bidx[rt][r] = 0x7fffffff;
+      bidx[rt][r] = 0;  // a row with no finite distance (NaN / inf in z) resolves to code 0, as tf.argmin
     }
 
   for (int k0 = 0; k0 < K; k0 += KC) {
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       best[rt][r] = __builtin_inff();
-      bidx[rt][r] = 0x7fffffff;
+      bidx[rt][r] = kbeg;  // no finite distance in this span: (inf, first code); the merge keeps code 0
     }
 
   for (int k0 = kbeg; k0 < kend; k0 += KC) {
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
       const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
       if ((lane & 15) == 0 && row < N) {
         if (packed) {
-          if (bi != 0x7fffffff) atomicMin((unsigned long long*)idx + row, vq_pack(b, bi));
+          atomicMin((unsigned long long*)idx + row, vq_pack(b, bi));
         } else {
           idx[row] = bi;
           if (mind) mind[row] = b;
@@ -327,12 +327,11 @@ __global__ __launch_bounds__(256) void vq_sqnorm_kernel(const float* E, float* e
   esq[k] = s;
 }
 
-// ---- quantize / straight-through / commitment / EMA sums ----------------------------------------
-// thread per (row, d); partial sums of (q - z)^2 per workgroup -> ws
+// ---- quantize / straight-through / commitment ----------------------------------------------------
+// thread per (row, d); partial sums of (q - z)^2 per workgroup -> ws (reduced in a fixed order)
 template <class T>
 __global__ __launch_bounds__(256) void vq_quantize_kernel(const T* z, const float* ET, const int64_t* idx, T* qst,
-                                                         float* m_sumT, float* n_sum, long long N, int D,
-                                                         float* ws) {
+                                                         long long N, int D, float* ws) {
   __shared__ float red[4];
   const long long total = N * D;
   float part = 0.f;
@@ -346,10 +345,6 @@ __global__ __launch_bounds__(256) void vq_quantize_kernel(const T* z, const floa
     const float diff = q - zf;
     part += diff * diff;
     st(qst + e, zf + diff);
-    if (m_sumT) {
-      atomicAdd(m_sumT + k * D + d, zf);
-      if (d == 0) atomicAdd(n_sum + k, 1.0f);
-    }
   }
   const float s = block_sum_256(part, red);
   if (threadIdx.x == 0) ws[blockIdx.x] = s;
@@ -449,73 +444,229 @@ static int quantize_blocks(long long total) {
 }
 
 // ---- EMA sums by code (VectorQuantizer.py:123-124: m_sum = z^T onehot, n_sum = column sums of onehot) ----
-// A per-row global atomic scatter serialises on the codes a batch crowds into (float atomics execute at the
-// memory side). Instead each workgroup owns a chunk of rows and a 16-channel slice and accumulates
-// [K][16] (+ the counts, slice 0) in LDS with LDS atomics; the chunk partials are then summed in a fixed
-// order by vqa_reduce_partials. Counts are exact; the channel sums are fp32 (LDS atomic order within a
-// chunk is not fixed, as with the global atomics this replaces).
-constexpr int kEmaSlice = 16;
-constexpr int kEmaChunks = 64;
-static bool ema_lds_ok(int D, int K) { return D % kEmaSlice == 0 && (size_t)K * (kEmaSlice + 1) * 4 <= 160 * 1024; }
-static int ema_chunks(long long N) {
-  long long c = (N + 4095) / 4096;
-  return (int)(c < kEmaChunks ? (c > 0 ? c : 1) : kEmaChunks);
+// Deterministic: the rows are counting-sorted by code (stable: by code, then row), and every code's sum is
+// taken over its rows in that order — sequential runs within 64-position tiles, tile partials added in tile
+// order. No floating-point atomics anywhere, so the sums (and the codebook they drive) are bitwise
+// reproducible run to run and independent of scheduling. Counts are exact integers.
+//   1 vq_sort_count_kernel   per 1024-row chunk: per-code counts, each row's rank among its chunk's equal codes
+//   2 vq_sort_scan_kernel    per code: exclusive prefix of the chunk counts; totals (n_sum += total)
+//   3 vq_sort_scatter_kernel segment starts (exclusive scan of the totals), perm[pos] = row, scode[pos] = code
+//   4 vq_seg_sum_kernel      one wave per 64 sorted positions, lanes = channels: run sums in row order; a run
+//                            that is its code's whole segment is added to m_sumT, others go to tile partials
+//   5 vq_seg_combine_kernel  codes spanning tiles: tile partials summed in tile order -> m_sumT
+constexpr int kSortChunk = 1024;  // rows per chunk (= threads of kernels 1 and 3)
+constexpr int kSegTile = 64;      // sorted positions per wave in kernel 4
+constexpr int kMaxSortK = 16384;  // LDS histogram bound (64 KB)
+
+struct SortWs {
+  int* cnt;    // [nch][K] chunk counts -> exclusive offsets within the code
+  int* tot;    // [K] rows per code
+  int* seg;    // [K + 1] segment starts in sorted order
+  int* lrank;  // [N] rank of the row among the equal codes of its chunk
+  int* perm;   // [N] sorted position -> row
+  int* scode;  // [N] sorted position -> code
+  float* tfirst;  // [ntile][D] sum of the tile's first run (when that run is not a whole segment)
+  float* tlast;   // [ntile][D] sum of the tile's last run (idem, when it is not also the first)
+};
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+static size_t sort_ws_bytes(long long N, int D, int K) {
+  const long long nch = (N + kSortChunk - 1) / kSortChunk, ntile = (N + kSegTile - 1) / kSegTile;
+  return align256((size_t)nch * K * 4) + align256((size_t)K * 4) + align256((size_t)(K + 1) * 4) +
+         3 * align256((size_t)N * 4) + 2 * align256((size_t)ntile * D * 4);
+}
+static SortWs sort_ws(void* base, long long N, int D, int K) {
+  const long long nch = (N + kSortChunk - 1) / kSortChunk, ntile = (N + kSegTile - 1) / kSegTile;
+  char* p = (char*)base;
+  SortWs w;
+  w.cnt = (int*)p;   p += align256((size_t)nch * K * 4);
+  w.tot = (int*)p;   p += align256((size_t)K * 4);
+  w.seg = (int*)p;   p += align256((size_t)(K + 1) * 4);
+  w.lrank = (int*)p; p += align256((size_t)N * 4);
+  w.perm = (int*)p;  p += align256((size_t)N * 4);
+  w.scode = (int*)p; p += align256((size_t)N * 4);
+  w.tfirst = (float*)p; p += align256((size_t)ntile * D * 4);
+  w.tlast = (float*)p;
+  return w;
 }
 
-constexpr int kEmaThreads = 1024;
-template <class T>
-__global__ __launch_bounds__(kEmaThreads) void vq_ema_sums_kernel(const T* z, const int64_t* idx, float* part, int N, int D,
-                                                          int K, int rows_per_chunk) {
-  extern __shared__ float tab[];  // [K][16] channel sums, then [K] counts
-  float* cnt = tab + K * kEmaSlice;
-  const int chunk = blockIdx.x, slice = blockIdx.y;
-  const bool counts = slice == 0;
-  const int nt = K * kEmaSlice + (counts ? K : 0);
-  for (int i = threadIdx.x; i < nt; i += kEmaThreads) tab[i] = 0.f;
+__global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t* idx, SortWs w, int N, int K) {
+  extern __shared__ int hist[];  // [K]
+  __shared__ __attribute__((aligned(16))) int codes[kSortChunk];
+  const int c = blockIdx.x, tid = threadIdx.x, row = c * kSortChunk + tid;
+  const int k = row < N ? (int)idx[row] : -1;
+  codes[tid] = k;
+  for (int i = tid; i < K; i += kSortChunk) hist[i] = 0;
   __syncthreads();
-  constexpr int RP = kEmaThreads / kEmaSlice;  // rows per pass
-  const int dl = threadIdx.x & (kEmaSlice - 1), rr = threadIdx.x / kEmaSlice;
-  const int r0 = chunk * rows_per_chunk, r1 = min(N, r0 + rows_per_chunk);
-  // each thread keeps a run (code, sum, count) in registers and adds it to the table only when the code
-  // changes: rows crowding into one code cost one LDS atomic per run, not per row
-  constexpr int U = 8;
-  int ck = -1;
-  float cs = 0.f, cc = 0.f;
-  for (int r = r0 + rr; r < r1; r += RP * U) {
-    int k[U];
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int ru = r + RP * u;
-      k[u] = ru < r1 ? (int)idx[ru] : -1;
-      v[u] = ru < r1 ? ld(z + (size_t)ru * D + slice * kEmaSlice + dl) : 0.f;
+  // stable rank: equal codes at lower rows of the chunk (wave-uniform trip count, 4 codes per LDS read)
+  const int wend = ((tid >> 6) + 1) * 64;
+  int r = 0;
+  for (int j = 0; j < wend; j += 4) {
+    const int4 q = *(const int4*)(codes + j);
+    r += (q.x == k && j < tid) + (q.y == k && j + 1 < tid) + (q.z == k && j + 2 < tid) + (q.w == k && j + 3 < tid);
+  }
+  if (row < N) {
+    w.lrank[row] = r;
+    atomicAdd(hist + k, 1);  // integer: order-independent
+  }
+  __syncthreads();
+  for (int i = tid; i < K; i += kSortChunk) w.cnt[(size_t)c * K + i] = hist[i];
+}
+
+// block = 16 waves x 64 codes: wave v scans its contiguous range of chunks, the 16 range totals are
+// prefixed in LDS, then each wave writes its range's exclusive offsets
+__global__ __launch_bounds__(1024) void vq_sort_scan_kernel(SortWs w, float* n_sum, int nch, int K) {
+  __shared__ int part[16][64];
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6, k = blockIdx.x * 64 + lane;
+  const int per = (nch + 15) / 16, c0 = min(nch, v * per), c1 = min(nch, c0 + per);
+  int s = 0;
+  if (k < K)
+    for (int c = c0; c < c1; ++c) s += w.cnt[(size_t)c * K + k];
+  part[v][lane] = s;
+  __syncthreads();
+  if (v == 0) {
+    int run = 0;
+    for (int i = 0; i < 16; ++i) {
+      const int t = part[i][lane];
+      part[i][lane] = run;
+      run += t;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (k[u] >= 0) {
-        if (k[u] != ck) {
-          if (ck >= 0) {
-            atomicAdd(tab + ck * kEmaSlice + dl, cs);
-            if (counts && dl == 0) atomicAdd(cnt + ck, cc);
-          }
-          ck = k[u];
-          cs = 0.f;
-          cc = 0.f;
-        }
-        cs += v[u];
-        cc += 1.f;
-      }
-  }
-  if (ck >= 0) {
-    atomicAdd(tab + ck * kEmaSlice + dl, cs);
-    if (counts && dl == 0) atomicAdd(cnt + ck, cc);
+    if (k < K) {
+      w.tot[k] = run;
+      n_sum[k] += (float)run;
+    }
   }
   __syncthreads();
-  float* out = part + (size_t)chunk * ((size_t)K * D + K);
-  for (int e = threadIdx.x; e < K * kEmaSlice; e += kEmaThreads)
-    out[(size_t)(e / kEmaSlice) * D + slice * kEmaSlice + (e % kEmaSlice)] = tab[e];
-  if (counts)
-    for (int e = threadIdx.x; e < K; e += kEmaThreads) out[(size_t)K * D + e] = cnt[e];
+  if (k < K) {
+    int run = part[v][lane];
+    for (int c = c0; c < c1; ++c) {
+      const int t = w.cnt[(size_t)c * K + k];
+      w.cnt[(size_t)c * K + k] = run;
+      run += t;
+    }
+  }
+}
+
+// exclusive scan of tot[0..K) into seg (LDS, K + 1 ints) by the block's 1024 threads
+__device__ void seg_scan(const int* tot, int* seg, int K) {
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, v = tid >> 6;
+  const int per = (K + kSortChunk - 1) / kSortChunk, i0 = min(K, tid * per), i1 = min(K, i0 + per);
+  int s = 0;
+  for (int i = i0; i < i1; ++i) s += tot[i];
+  int incl = s;  // inclusive wave scan
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[v] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < v; ++i) base += wsum[i];
+  int run = base + incl - s;
+  for (int i = i0; i < i1; ++i) {
+    seg[i] = run;
+    run += tot[i];
+  }
+  if (tid == kSortChunk - 1) seg[K] = run;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSortChunk) void vq_sort_scatter_kernel(const int64_t* idx, SortWs w, int N, int K) {
+  extern __shared__ int seg[];  // [K + 1]
+  seg_scan(w.tot, seg, K);
+  const int c = blockIdx.x, row = c * kSortChunk + threadIdx.x;
+  if (c == 0)
+    for (int i = threadIdx.x; i <= K; i += kSortChunk) w.seg[i] = seg[i];
+  if (row >= N) return;
+  const int k = (int)idx[row];
+  const int pos = seg[k] + w.cnt[(size_t)c * K + k] + w.lrank[row];
+  w.perm[pos] = row;
+  w.scode[pos] = k;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void vq_seg_sum_kernel(const T* z, SortWs w, float* m_sumT, int N, int D) {
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p0 = tile * kSegTile;
+  if (p0 >= N) return;
+  const int np = min(kSegTile, N - p0);
+  const int myrow = lane < np ? w.perm[p0 + lane] : 0;
+  const int mycode = lane < np ? w.scode[p0 + lane] : -1;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    const bool on = d < D;
+    float v[kSegTile];
+#pragma unroll
+    for (int i = 0; i < kSegTile; ++i) {
+      const int row = __builtin_amdgcn_readlane(myrow, i);
+      v[i] = (on && i < np) ? ld(z + (size_t)row * D + d) : 0.f;
+    }
+    float s = 0.f;
+    int a = 0;
+#pragma unroll
+    for (int i = 0; i < kSegTile; ++i) {
+      if (i >= np) continue;  // uniform (partial last tile); keeps the loop unrolled (v[] in registers)
+      s += v[i];
+      const int k = __builtin_amdgcn_readlane(mycode, i);
+      const int kn = i + 1 < np ? __builtin_amdgcn_readlane(mycode, i + 1) : -1;
+      if (kn != k) {  // run [a, i] of code k ends
+        const int S = w.seg[k], E = w.seg[k + 1];
+        if (on) {
+          if (S >= p0 && E <= p0 + np) m_sumT[(size_t)k * D + d] += s;       // whole segment in this tile
+          else if (a == 0) w.tfirst[(size_t)tile * D + d] = s;                // segment continues across a tile edge
+          else w.tlast[(size_t)tile * D + d] = s;
+        }
+        s = 0.f;
+        a = i + 1;
+      }
+    }
+  }
+}
+
+// one workgroup (4 waves) per code whose segment spans several tiles: the waves sum contiguous quarters of
+// the tile range in order, then the quarters are added in order (a fixed tree for a given segment)
+__global__ __launch_bounds__(256) void vq_seg_combine_kernel(SortWs w, float* m_sumT, int D) {
+  __shared__ float q[4][64];
+  const int k = blockIdx.x, lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int S = w.seg[k], E = w.seg[k + 1];
+  if (E <= S) return;
+  const int ta = S / kSegTile, tb = (E - 1) / kSegTile;
+  if (ta == tb) return;  // whole segment inside one tile: added by vq_seg_sum_kernel
+  const int n = tb - ta;  // tiles ta+1 .. tb read tfirst
+  const int per = (n + 3) / 4, i0 = ta + 1 + min(n, v * per), i1 = ta + 1 + min(n, (v + 1) * per);
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    float s = 0.f;
+    if (d < D) {
+      if (v == 0) s = (S == ta * kSegTile ? w.tfirst : w.tlast)[(size_t)ta * D + d];
+      for (int t = i0; t < i1; ++t) s += w.tfirst[(size_t)t * D + d];
+    }
+    q[v][lane] = s;
+    __syncthreads();
+    if (v == 0 && d < D) m_sumT[(size_t)k * D + d] += ((q[0][lane] + q[1][lane]) + q[2][lane]) + q[3][lane];
+    __syncthreads();
+  }
+}
+
+template <class T>
+static int launch_ema_sums(const T* z, const int64_t* idx, float* m_sumT, float* n_sum, long long N, int D, int K,
+                           void* ws, hipStream_t s) {
+  const int nch = (int)((N + kSortChunk - 1) / kSortChunk), ntile = (int)((N + kSegTile - 1) / kSegTile);
+  const SortWs w = sort_ws(ws, N, D, K);
+  hipLaunchKernelGGL(vq_sort_count_kernel, dim3(nch), dim3(kSortChunk), (size_t)K * 4, s, idx, w, (int)N, K);
+  VQA_LAUNCHED("vq_sort_count_kernel");
+  hipLaunchKernelGGL(vq_sort_scan_kernel, dim3((K + 63) / 64), dim3(1024), 0, s, w, n_sum, nch, K);
+  VQA_LAUNCHED("vq_sort_scan_kernel");
+  hipLaunchKernelGGL(vq_sort_scatter_kernel, dim3(nch), dim3(kSortChunk), (size_t)(K + 1) * 4, s, idx, w, (int)N, K);
+  VQA_LAUNCHED("vq_sort_scatter_kernel");
+  hipLaunchKernelGGL(vq_seg_sum_kernel<T>, dim3((ntile + 3) / 4), dim3(256), 0, s, z, w, m_sumT, (int)N, D);
+  VQA_LAUNCHED("vq_seg_sum_kernel");
+  hipLaunchKernelGGL(vq_seg_combine_kernel, dim3(K), dim3(256), 0, s, w, m_sumT, D);
+  VQA_LAUNCHED("vq_seg_combine_kernel");
+  return VQA_OK;
 }
 
 }  // namespace vqa
@@ -598,8 +749,7 @@ extern "C" int vqa_vq_argmin_split(const void* z, const void* E3, const float* e
 
 extern "C" size_t vqa_vq_quantize_workspace(int64_t N, int D, int K, int dtype) {
   (void)dtype;
-  const size_t head = ((size_t)quantize_blocks((long long)N * D) * sizeof(float) + 255) & ~(size_t)255;
-  return head + (ema_lds_ok(D, K) ? (size_t)ema_chunks(N) * ((size_t)K * D + K) * sizeof(float) : 0);
+  return align256((size_t)quantize_blocks((long long)N * D) * sizeof(float)) + sort_ws_bytes(N, D, K);
 }
 
 extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* idx, void* q_st, float* commit_out,
@@ -610,46 +760,24 @@ extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* id
   VQA_ARG(N > 0 && D > 0 && K > 0, "vq_quantize: bad shape");
   const int nb = quantize_blocks((long long)N * D);
   VQA_ARG(dtype == VQA_BF16 || dtype == VQA_F32, "vq_quantize: unknown dtype %d", dtype);
-  VQA_ARG(N < (1ll << 31) && D <= 64, "vq_quantize: N=%lld D=%d out of range", (long long)N, D);
+  VQA_ARG(N < (1ll << 31) - kSortChunk && D <= 1024 && K <= kMaxSortK, "vq_quantize: N=%lld D=%d K=%d out of range",
+          (long long)N, D, K);
   VQA_ARG(workspace && ws_bytes >= vqa_vq_quantize_workspace(N, D, K, dtype), "vq_quantize: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  // q, straight-through output and the commitment partials; EMA sums here only when they do not fit the
-  // LDS-table path below
-  const bool lds = m_sumT && ema_lds_ok(D, K);
-  float* ms = lds ? nullptr : m_sumT;
-  float* ns = lds ? nullptr : n_sum;
+  // q, straight-through output and the commitment partials
   if (dtype == VQA_BF16)
-    hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st, ms,
-                       ns, (long long)N, D, (float*)workspace);
+    hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st,
+                       (long long)N, D, (float*)workspace);
   else
     hipLaunchKernelGGL(vq_quantize_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)z, ET, idx, (float*)q_st,
-                       ms, ns, (long long)N, D, (float*)workspace);
+                       (long long)N, D, (float*)workspace);
   VQA_LAUNCHED("vq_quantize_kernel");
-  if (lds) {
-    const int nch = ema_chunks(N), rpc = (int)((N + nch - 1) / nch);
-    float* part = (float*)((char*)workspace + (((size_t)nb * sizeof(float) + 255) & ~(size_t)255));
-    const size_t lds_bytes = (size_t)K * (kEmaSlice + 1) * sizeof(float);
-    const void* fn = dtype == VQA_BF16 ? (const void*)vq_ema_sums_kernel<bf16> : (const void*)vq_ema_sums_kernel<float>;
-    static size_t lds_set[2] = {0, 0};
-    size_t& cached = lds_set[dtype == VQA_BF16 ? 0 : 1];
-    if (lds_bytes > 65536 && lds_bytes > cached) {
-      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        set_error("vq_quantize: cannot reserve %zu B of LDS", lds_bytes);
-        return VQA_E_UNSUPPORTED;
-      }
-      cached = lds_bytes;
-    }
-    const dim3 grid(nch, D / kEmaSlice);
-    if (dtype == VQA_BF16)
-      hipLaunchKernelGGL(vq_ema_sums_kernel<bf16>, grid, dim3(kEmaThreads), lds_bytes, s, (const bf16*)z, idx, part, (int)N, D,
-                         K, rpc);
-    else
-      hipLaunchKernelGGL(vq_ema_sums_kernel<float>, grid, dim3(kEmaThreads), lds_bytes, s, (const float*)z, idx, part, (int)N,
-                         D, K, rpc);
-    VQA_LAUNCHED("vq_ema_sums_kernel");
-    const vqa_partials_desc d{part, m_sumT, n_sum, nch, K * D + K, K * D, 0};
-    if (int rc = vqa_reduce_partials(&d, 1, stream)) return rc;
+  if (m_sumT) {
+    void* sws = (char*)workspace + align256((size_t)nb * sizeof(float));
+    const int rc = dtype == VQA_BF16
+                       ? launch_ema_sums<bf16>((const bf16*)z, idx, m_sumT, n_sum, N, D, K, sws, s)
+                       : launch_ema_sums<float>((const float*)z, idx, m_sumT, n_sum, N, D, K, sws, s);
+    if (rc) return rc;
   }
   // beta * mean((q - z)^2) over N*D elements (VectorQuantizer.py:97-99)
   const float scale = (float)((double)beta / ((double)N * (double)D));

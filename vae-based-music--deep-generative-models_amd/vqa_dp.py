@@ -49,7 +49,15 @@ def exchange(bucket: torch.Tensor, group=None) -> int:
     """Sum the bucket over ranks (no-op on one rank). Returns the world size (grad scale = 1/W)."""
     w = world_size(group)
     if w > 1:
-        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
+        if bucket.is_cuda and dist.get_backend(group) != "nccl":
+            # host backends (gloo: the CPU rehearsal / tests of the DP path): stage through host memory
+            # explicitly, ordered after every kernel that wrote the bucket
+            torch.cuda.current_stream(bucket.device).synchronize()
+            host = bucket.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            bucket.copy_(host)
+        else:
+            dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)  # RCCL over xGMI
     return w
 
 

@@ -33,6 +33,7 @@ EXPORTED = [
     "vqa_resblock_supported", "vqa_resblock_fwd", "vqa_resblock_bwd", "vqa_resblock_bwd_workspace",
     "vqa_spectral_target_workspace", "vqa_spectral_target", "vqa_spectral_loss_target_workspace",
     "vqa_spectral_loss_target", "vqa_dtail_supported", "vqa_dtail_workspace", "vqa_dtail_fwd", "vqa_dtail_bwd",
+    "vqa_step_metrics",
 ]
 
 
@@ -76,6 +77,7 @@ _SIGS = {
     "vqa_mse_loss_workspace": (_S, [_L]),
     "vqa_adam_keras": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P]),
     "vqa_counter_add": (_I, [_P, _L, _P]),
+    "vqa_step_metrics": (_I, [_P, _P, _P, _I, _F, _P]),
     "vqa_conv1d_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
     "vqa_conv1d_transpose_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONVT + [_P, _S, _P, _P]),
     "vqa_reduce_partials": (_I, [_P, _I, _P]),
@@ -378,6 +380,11 @@ def mse_loss(x, r, extra, dr, loss_out):
 def adam_keras(w, g, m, v, step, lr, beta1, beta2, eps, grad_scale):
     _check(lib().vqa_adam_keras(ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), ptr(step), lr, beta1, beta2, eps,
                                 grad_scale, stream()), "vqa_adam_keras")
+
+
+def step_metrics(loss_slots, vq_metrics, macc, levels, scale):
+    _check(lib().vqa_step_metrics(ptr(loss_slots), ptr(vq_metrics), ptr(macc), levels, scale, stream()),
+           "vqa_step_metrics")
 
 
 def counter_add(counter, delta=1):

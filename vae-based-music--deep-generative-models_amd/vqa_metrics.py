@@ -1,4 +1,10 @@
-"""keras.metrics.Mean equivalent kept on the device (no host sync per step; graph-capturable)."""
+"""keras.metrics.Mean equivalents kept on the device (no host sync per step; graph-capturable).
+
+`Mean` owns its (total, count) pair. `SlotMean` is a tracker over one row of a model-owned accumulator
+(the VQVAE keeps every tracker of a step in one (n, 2) tensor that a single libvqa launch updates,
+vqa_step_metrics); both expose the Keras tracker surface the reference's callers use: `.name`,
+`.update_state(v)`, `.result()`, `.reset_state()` (src/callback/vae_monitor.py:64-65,71).
+"""
 from __future__ import annotations
 
 import torch
@@ -18,3 +24,14 @@ class Mean:
 
     def reset_state(self):
         self._acc.zero_()
+
+    # keras 2.x alias
+    reset_states = reset_state
+
+
+class SlotMean(Mean):
+    """Mean over row `row` of a shared (n, 2) [total, count] accumulator."""
+
+    def __init__(self, name: str, acc: torch.Tensor, row: int):
+        self.name = name
+        self._acc = acc[row]

@@ -31,7 +31,7 @@ import vqa_lib as V
 from data_utils import SpectralTarget, multispectral_loss_and_grad
 from encdec import Decoder, Encoder
 from vqa_layers import ParamStore
-from vqa_metrics import Mean
+from vqa_metrics import SlotMean
 from vqa_optim import Adam
 from VectorQuantizer import VectorQuantizer
 
@@ -44,29 +44,57 @@ def _dtype(d) -> torch.dtype:
     raise ValueError(f"unsupported compute dtype {d}")
 
 
-class _LevelModel:
-    """Stands in for the per-level keras.Model of get_vqvae (vqvae.py:15-21): x -> enc -> vq -> dec."""
+class LevelModel:
+    """The per-level keras.Model of get_vqvae (vqvae.py:15-21): x -> encoder -> vq -> decoder on an input of
+    fixed shape `input_shape` (keras.Input). Inside a VQVAE it runs on the model's kernels and buffers
+    (`vqvaes[level]`); from get_vqvae it owns a parameter store of its own."""
 
-    def __init__(self, owner: "VQVAE", level: int):
-        self.owner, self.level = owner, level
+    def __init__(self, input_shape, encoder, decoder, vq, level=0, owner: Optional["VQVAE"] = None,
+                 dtype="fp32", device=None, seed=1):
+        self.input_shape = tuple(input_shape)
+        self.encoder, self.decoder, self.vq, self.level, self.owner = encoder, decoder, vq, level, owner
         self.name = f"vq_vae_{level}"
+        if owner is None:
+            self.cdt = _dtype(dtype)
+            self.device = torch.device(device) if device is not None else vq.device
+            self.store = ParamStore()
+            if not encoder.built:
+                encoder.build(self.store, f"enc{level}", int(self.input_shape[-1]), self.cdt)
+            if not decoder.built:
+                decoder.build(self.store, f"dec{level}", vq.embedding_dim, self.cdt)
+            self.store.materialize(self.device, seed=seed)
 
     def __call__(self, x, training=True):
-        return self.owner._level_forward_only(self.owner._as_input(x), self.level, training)
+        if self.owner is not None:
+            return self.owner._level_forward_only(self.owner._as_input(x), self.level, training)
+        x = x[0] if isinstance(x, (tuple, list)) else x
+        x = torch.as_tensor(x).to(device=self.device, dtype=torch.float32)
+        if x.dim() == 2:
+            x = x.unsqueeze(-1)
+        if tuple(x.shape[1:]) != self.input_shape:
+            raise ValueError(f"input shape {tuple(x.shape)} does not match keras.Input{self.input_shape}")
+        with torch.no_grad():
+            z = self.encoder.forward(x.contiguous())
+            q, _ = self.vq.call(z, training=training)
+            return self.decoder.forward(q)
+
+    call = __call__
 
     @property
     def losses(self):
-        return self.owner.vqs[self.level].losses
+        return self.vq.losses
 
     @property
     def trainable_variables(self):
-        o = self.owner
-        return [o.store.view(n) for n, _, _ in o.store.specs if n.startswith((f"enc{self.level}/", f"dec{self.level}/"))]
+        st = self.owner.store if self.owner is not None else self.store
+        pre = (f"enc{self.level}/", f"dec{self.level}/")
+        return [st.view(n) for n, _, _ in st.specs if n.startswith(pre)]
 
 
-def get_vqvae(input_shape, encoder, decoder, vq, level=0):
-    """vqvae.py:15-21 — provided for API parity; VQVAE builds its levels itself."""
-    raise NotImplementedError("build a VQVAE; its .vqvaes[level] are the per-level models")
+def get_vqvae(input_shape, encoder, decoder, vq, level=0, **kwargs):
+    """vqvae.py:15-21 — the single-level model x -> encoder -> vq -> decoder (keras default init of the
+    encoder / decoder weights unless they are already built)."""
+    return LevelModel(input_shape, encoder, decoder, vq, level, **kwargs)
 
 
 class VQVAE:
@@ -123,15 +151,30 @@ class VQVAE:
         for l, vq in enumerate(self.vqs):
             vq.commit = self.loss_slots[l, 1:2]
 
-        # metric trackers (vqvae.py:77-89 + VectorQuantizer.py:62-64), one device accumulator
+        # metric trackers (vqvae.py:77-89 + VectorQuantizer.py:62-64): ONE device accumulator, rows in the
+        # order of the returned dict (update_metrics, vqvae.py:262-304), updated by one vqa_step_metrics launch
         names = ["loss", "recon_loss", "vqvae_loss", "spectral_loss"]
         for l in range(levels):
             names += [f"[{l}]level_loss", f"[{l}]recon_loss", f"[{l}]vq_loss", f"[{l}]spectral_loss",
                       f"[{l}]batch_codebook_usage", f"[{l}]codebook_usage", f"[{l}]codebook_entropy"]
         self.metric_names = names
         self._macc = torch.zeros(len(names), 2, dtype=torch.float32, device=self.device)
+        self._vq_metrics = torch.zeros(levels, 3, dtype=torch.float32, device=self.device)
+        row = {n: i for i, n in enumerate(names)}
+        # keras.metrics.Mean trackers with the reference's names (vqvae.py:78-89), views of _macc rows
+        self.total_loss_tracker = SlotMean("total_loss", self._macc, row["loss"])
+        self.reconstruction_loss_tracker = SlotMean("reconstruction_loss", self._macc, row["recon_loss"])
+        self.vq_loss_tracker = SlotMean("vq_loss", self._macc, row["vqvae_loss"])
+        self.spectral_loss_tracker = SlotMean("spectral_loss", self._macc, row["spectral_loss"])
+        self.level_loss_trackers, self.recon_loss_trackers, self.vq_loss_trackers, self.spectral_loss_trackers = (
+            [SlotMean(f"[{l}]{k}", self._macc, row[f"[{l}]{k}"]) for l in range(levels)]
+            for k in ("level_loss", "recon_loss", "vq_loss", "spectral_loss"))
+        for l, vq in enumerate(self.vqs):
+            vq.bind_metrics(self._vq_metrics[l], self._macc,
+                            [row[f"[{l}]{k}"] for k in ("batch_codebook_usage", "codebook_usage", "codebook_entropy")])
         self.optimizer: Optional[Adam] = None
-        self.vqvaes = [_LevelModel(self, l) for l in range(levels)]
+        self.vqvaes = [LevelModel(self.input_shape, self.encoders[l], self.decoders[l], self.vqs[l], l, owner=self)
+                       for l in range(levels)]
         self._graph = None
         # run the levels' independent forward/backward chains on one stream each (VQA_LEVEL_STREAMS=0: serial)
         self.concurrent_levels = os.environ.get("VQA_LEVEL_STREAMS", "1") != "0"
@@ -144,13 +187,18 @@ class VQVAE:
 
     @property
     def metrics(self):
-        return list(self.metric_names)
+        """vqvae.py:93-104: the model's keras Mean trackers (total, reconstruction, vq, spectral, then the
+        per-level level / recon / vq / spectral trackers). `for m in model.metrics: m.reset_state()`
+        (src/callback/vae_monitor.py:64-65) and `m.name`, `m.result()` (:71) work unchanged."""
+        return [self.total_loss_tracker, self.reconstruction_loss_tracker, self.vq_loss_tracker,
+                self.spectral_loss_tracker, *self.level_loss_trackers, *self.recon_loss_trackers,
+                *self.vq_loss_trackers, *self.spectral_loss_trackers]
 
     def reset_metrics(self):
-        self._macc.zero_()
-        for vq in self.vqs:
-            for m in vq.metrics:
-                m.reset_state()
+        """keras Model.reset_metrics: resets `self.metrics` only. The codebook usage / entropy trackers are
+        not in that list (VectorQuantizer.metrics), so, as in the reference, they keep accumulating."""
+        for m in self.metrics:
+            m.reset_state()
 
     def get_quantizer(self):
         return self.vqs[0]
@@ -226,15 +274,13 @@ class VQVAE:
             self.optimizer.apply(self.store, grad_scale=1.0 / world)
         for vq in self.vqs:
             vq.apply_ema(update_trackers=False)
-        vals = self.loss_slots * (1.0 / world)
-        lvl = vals.sum(dim=1)
-        tot = torch.cat([lvl.sum().reshape(1), vals.sum(dim=0)])
-        per = torch.cat([lvl.reshape(-1, 1), vals, torch.stack([vq.vq_metrics for vq in self.vqs])], dim=1)
-        self._macc[:, 0] += torch.cat([tot, per.reshape(-1)])
-        self._macc[:, 1] += 1.0
+        # update_metrics (vqvae.py:262-304) + the VQ trackers: one launch
+        V.step_metrics(self.loss_slots, self._vq_metrics, self._macc, self.levels, 1.0 / world)
 
-    def _exchange(self):
-        vqa_dp.exchange(self.bucket, self.process_group)
+    def _exchange(self, grads: bool = True):
+        """The step's one collective: all_reduce(SUM) of [grads | EMA sums | reset rows | losses]; without
+        gradients (test_step) only the statistics region."""
+        vqa_dp.exchange(self.bucket if grads else self._stats_region, self.process_group)
 
     def results(self) -> Dict[str, torch.Tensor]:
         res = self._macc[:, 0] / self._macc[:, 1].clamp(min=1.0)
@@ -259,7 +305,7 @@ class VQVAE:
         x = self._as_input(data)
         with torch.no_grad():
             self._compute(x, training_grads=False)
-            self._exchange()
+            self._exchange(grads=False)
             self._update(apply_grads=False)
         return self.results()
 
@@ -304,13 +350,21 @@ class VQVAE:
 
     # ------------------------------------------------------------------ inference API
     def _level_forward_only(self, x, l, training):
+        """vqvaes[l](x, training): forward of one level; with training the VQ EMA runs (VectorQuantizer.py:
+        116-145) — under data parallelism on the statistics of the GLOBAL batch (this level's region of the
+        bucket is all-reduced first), so the replicas' codebooks stay identical."""
+        vq = self.vqs[l]
         with torch.no_grad():
             z = self.encoders[l].forward(x)
             if training:
-                self.vqs[l].stats.zero_()
-            q, _ = self.vqs[l].forward(z, training=training)
-            if training:
-                self.vqs[l].apply_ema()
+                vq.stats.zero_()
+                n_loc = z.shape[0] * z.shape[1]
+                row_offset, n_global = vqa_dp.global_row_range(n_loc, self.process_group)
+                q, _ = vq.forward(z, training=True, row_offset=row_offset, n_global=n_global)
+                vqa_dp.exchange(vq.stats, self.process_group)
+                vq.apply_ema()
+            else:
+                q, _ = vq.forward(z, training=False)
             return self.decoders[l].forward(q)
 
     def __call__(self, x, training=False):
@@ -360,7 +414,8 @@ class VQVAE:
 
     # ------------------------------------------------------------------ training loop / state
     def fit(self, x=None, y=None, batch_size=32, epochs=1, shuffle=True, seed=0, verbose=0):
-        """Minimal keras fit: metrics reset per epoch; returns history of epoch-end results."""
+        """Minimal keras fit: `self.metrics` reset per epoch (keras semantics); returns the history of
+        epoch-end results."""
         if self.optimizer is None:
             self.compile()
         xs = np.asarray(x, np.float32)
@@ -402,6 +457,41 @@ class VQVAE:
             sd.update({"adam_m": self.optimizer.m.cpu().clone(), "adam_v": self.optimizer.v.cpu().clone(),
                        "iterations": int(self.optimizer.iterations.item())})
         return sd
+
+    def save(self, path: str):
+        """Checkpoint to disk (the reference saves through an injected tf.train.CheckpointManager every
+        ckpt_interval epochs, src/callback/vae_monitor.py:56-58): tensors, ints and strings only, so
+        `torch.load(path, weights_only=True)` reads it. Holds the weights, Adam moments and step, and each
+        level's codebook E, m_t, N_t and reset counter: resuming reproduces the uninterrupted run bit for
+        bit (every reduction of the step runs in a fixed order)."""
+        sd = self.state_dict()
+        out = {"format": "vqa-vqvae/1", "param_names": [n for n, _, _ in self.store.specs],
+               "config": {"input_shape": list(self.input_shape), "levels": self.levels,
+                          "latent_dim": self.latent_dim, "num_embeddings": self.num_embeddings,
+                          "down_depth": list(self.down_depth), "strides": list(self.strides)},
+               "weights": sd["weights"]}
+        for k in ("adam_m", "adam_v", "iterations"):
+            if k in sd:
+                out[k] = sd[k]
+        for l, st in enumerate(sd["vq"]):
+            for k in ("embeddings", "m_t", "N_t"):
+                out[f"vq{l}/{k}"] = torch.from_numpy(np.ascontiguousarray(st[k]))
+            out[f"vq{l}/calls"] = int(st["calls"])
+        torch.save(out, path)
+
+    def load(self, path: str):
+        """Restore a `save` checkpoint (loaded weights-only: nothing in the file is executed)."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        if ck.get("format") != "vqa-vqvae/1":
+            raise ValueError(f"{path}: not a vqa-vqvae/1 checkpoint")
+        if ck["param_names"] != [n for n, _, _ in self.store.specs]:
+            raise ValueError(f"{path}: parameter layout differs from this model's")
+        sd = {"weights": ck["weights"], "vq": [{k: ck[f"vq{l}/{k}"].numpy() for k in ("embeddings", "m_t", "N_t")}
+                                               | {"calls": ck[f"vq{l}/calls"]} for l in range(self.levels)]}
+        for k in ("adam_m", "adam_v", "iterations"):
+            if k in ck:
+                sd[k] = ck[k]
+        self.load_state_dict(sd)
 
     def load_state_dict(self, sd):
         self.store.flat.copy_(sd["weights"].to(self.device))
