@@ -34,9 +34,10 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "audio-samples/sec/GPU VQ-VAE train step, 44.1kHz 65536-frame chunks @1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
 CFG2 = dict(levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2], num_embeddings=2048,
             residual_width=32, residual_depth=4, dilation_factor=3)
-DOMINANT = "resblock_bwd_kernel<bf16>"  # fused residual-block backward (h recomputed): 104 launches per step
+DOMINANT = "resblock_bwd_kernel<bf16>"  # fused residual-block backward (h recomputed): 120 launches per step
 
 
 def parse():
@@ -72,7 +73,13 @@ class KernelTimer:
     def __init__(self, V):
         self.V = V
         self.calls = []
+        self.rows = []
         self.orig = None
+
+    def flops_per_step(self) -> float:
+        """Algorithmic MFMA flops of the step's launches: five k=3, 32->32 convs (h recompute, dW_b, dh, dx,
+        dW_a), 2*3*32*32 flop per row each, over the B*T rows (the halo recompute is not counted)."""
+        return float(sum(5 * 2 * 3 * 32 * 32 * B * T for B, T, _ in self.rows))
 
     def __enter__(self):
         self.orig = f = self.V.resblock_bwd
@@ -80,6 +87,7 @@ class KernelTimer:
         def wrapped(dy, x, *rest, _f=f):
             unit = x.numel() * x.element_size()
             self.calls.append(((dy, x) + tuple(rest), 8 * unit, 3 * unit))
+            self.rows.append((x.shape[0], x.shape[1], rest[-2]))  # (B, T, dilation)
             return _f(dy, x, *rest)
         self.V.resblock_bwd = wrapped
         return self
@@ -113,9 +121,23 @@ class KernelTimer:
         return n, us_total, sum(c[1] for c in self.calls), sum(c[2] for c in self.calls)
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
 def cpu_baseline(batch, steps, seq):
+    """The oracle (reference op sequence, fp32) on the host cores this process may use: every CPU of its
+    affinity mask, capped by OMP_NUM_THREADS when the box sets its CPU share that way (16 per GPU)."""
     from oracle import vqvae_ref as R
-    threads = min(16, os.cpu_count() or 1)
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(allowed, omp) if omp > 0 else allowed
     torch.set_num_threads(threads)
     cfg = R.RefConfig(input_len=seq, **CFG2)
     m = R.RefVQVAE(cfg, R.init_params(cfg, 1), R.init_vq_state(cfg, 2), dtype=torch.float32)
@@ -126,9 +148,11 @@ def cpu_baseline(batch, steps, seq):
         m.train_step(x)
     dt = time.perf_counter() - t0
     return {"value": batch * seq * steps / dt, "unit": "audio-samples/s", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": allowed,
             "sample": f"oracle torch-CPU fp32 train step (dense one-hot GEMMs, N x K distances, TF-style STFT) on "
                       f"the cfg2 architecture, {batch} x {seq}-frame chunks, {steps} timed steps after 1 warm-up, "
-                      f"{threads} threads ({dt:.1f} s)"}
+                      f"{threads} threads of {_cpu_model()} (nproc {os.cpu_count()}, {allowed} in this process's "
+                      f"affinity mask, OMP_NUM_THREADS {omp or 'unset'}; {dt:.1f} s)"}
 
 
 def main():
@@ -149,13 +173,13 @@ def main():
         else:
             dist.init_process_group(backend)
     import vqa_lib as V
-    from data_utils import synthetic_batch
+    from data_utils import synthetic_batch_device
     from vqvae import VQVAE
 
     model = VQVAE((a.seq, 1), dtype=a.dtype, device=dev, **CFG2)
     model.compile()
-    batches = [torch.from_numpy(synthetic_batch(a.batch, a.seq, seed=1234 + rank + 7919 * i)).to(dev)
-               for i in range(4)]
+    # the device feed: 4 batches generated in HBM by vqa_synthetic_batch (seeded per rank)
+    batches = [synthetic_batch_device(a.batch, a.seq, seed=1234 + 7919 * i, rank=rank, device=dev) for i in range(4)]
     if not a.no_graph:
         # 1 eager step (FFT plans, LDS limits), capture, then warmup-1 untimed replays: the first replays
         # of a fresh hipGraph carry its upload cost
@@ -188,30 +212,47 @@ def main():
     n_launch, us_total, nbytes, cbytes = (0, 0.0, 0, 0) if a.no_roofline else kt.measure()
     achieved = nbytes / (us_total * 1e-6) / 1e9 if us_total > 0 else 0.0
     compulsory = cbytes / (us_total * 1e-6) / 1e9 if us_total > 0 else 0.0
-    traffic = None
+    pmc = {}
     if os.path.exists(a.pmc_json):
         try:
-            traffic = json.load(open(a.pmc_json)).get("per_launch_bytes")
+            pmc = json.load(open(a.pmc_json))
         except Exception:
-            traffic = None
+            pmc = {}
+    traffic = pmc.get("per_launch_bytes")
+    avg_us = us_total / max(n_launch, 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": DOMINANT,
-            "launches_per_step": n_launch, "avg_launch_us": round(us_total / max(n_launch, 1), 2),
+            "launches_per_step": n_launch, "avg_launch_us": round(avg_us, 2),
             "algorithmic_bytes_per_launch": int(nbytes / max(n_launch, 1)),
             "compulsory_bytes_per_launch": int(cbytes / max(n_launch, 1)),
-            "compulsory_GBps": round(compulsory, 1),
+            "compulsory_GBps": round(compulsory, 1), "compulsory_frac": round(compulsory / HBM_PEAK_GBS, 4),
             "kernel_ms_per_step": round(us_total / 1e3, 3)}
+    if traffic and avg_us > 0:
+        # measured HBM bytes (PMC, profiles/) over the live average launch time: the real bandwidth fraction
+        roof["traffic_GBps"] = round(traffic / (avg_us * 1e-6) / 1e9, 1)
+        roof["traffic_frac"] = round(traffic / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    if n_launch:
+        # MFMA: the launch's matrix flops (5 k=3 convs over the tile rows incl. the recomputed halo) against
+        # the dense bf16 peak, and the PMC busy fraction (SQ_VALU_MFMA_BUSY_CYCLES) when measured
+        fl = kt.flops_per_step()
+        roof["mfma"] = {"tflops": round(fl / (us_total * 1e-6) / 1e12, 1), "peak_tflops": BF16_DENSE_TFLOPS,
+                        "frac": round(fl / (us_total * 1e-6) / 1e12 / BF16_DENSE_TFLOPS, 4),
+                        "busy_frac_pmc": pmc.get("mfma_busy_frac")}
 
     out = None
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.cpu_batch, a.cpu_steps, a.seq)
+        # value: the whole job's audio-samples/s (all ranks; the driver derives scaling from it);
+        # value_per_gpu: the metric's per-GPU reading (B_per_gpu * T * steps / wall-seconds)
         value = a.batch * a.seq * a.steps * world / elapsed
-        out = {"metric": METRIC, "value": round(value, 1), "unit": "audio-samples/s", "n_gpus": world,
+        out = {"metric": METRIC, "value": round(value, 1), "value_per_gpu": round(value / world, 1),
+               "unit": "audio-samples/s", "n_gpus": world,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-               "data": "synthetic 44.1 kHz sine+noise chunks (SURVEY.md §8d), random-init weights",
+               "data": "synthetic 44.1 kHz sine+noise chunks (SURVEY.md §8d) generated on the device "
+                       "(vqa_synthetic_batch), random-init weights",
                "config": {"workload": "SMALL_VQ_VAE 3-level VQ-VAE train step (BASELINE config 2)",
                           "model": "VQVAE levels=3 latent=64 K=2048 down_depth=[3,2,2] width=32 depth=4 dil=3",
                           "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",

@@ -213,6 +213,11 @@ int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, cons
  * levels x 3 (vqa_vq_ema_apply's metrics). Each row gets total += value, count += 1 (keras Mean). */
 int vqa_step_metrics(const float* loss_slots, const float* vq_metrics, float* macc, int levels, float scale,
                      vqa_stream_t stream);
+/* On-device synthetic feed (replaces the host chunk feed of data_utils.py:65-206 and the
+ * notebook tf.data pipeline): x (B, T) fp32 = clip(0.5 sin(2 pi f_b t / sr + phi_b) + 0.05 N(0,1), -1, 1) with
+ * f_b ~ U[55, 2000) Hz, phi_b ~ U[0, 2 pi); counter-based draws keyed by (seed, rank, item, sample). */
+int vqa_synthetic_batch(float* x, int B, int64_t T, uint64_t seed, int rank, float sample_rate,
+                        vqa_stream_t stream);
 /* *counter += delta on the stream (graph-capturable step counters). */
 int vqa_counter_add(int64_t* counter, int64_t delta, vqa_stream_t stream);
 

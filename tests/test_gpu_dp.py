@@ -66,10 +66,13 @@ def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode):
     ranks = _run_ranks(mode, tmp_path)
     ref = _single()
     K, D = W.CFG["num_embeddings"], W.CFG["latent_dim"]
+    assert torch.equal(ranks[0]["steps"]["stats"], ranks[1]["steps"]["stats"])  # incl. the exchanged losses
     for phase in ("steps", "forward"):
         r0, r1, s = ranks[0][phase], ranks[1][phase], ref[phase]
-        # replicas identical
-        assert torch.equal(r0["weights"], r1["weights"]) and torch.equal(r0["stats"], r1["stats"])
+        # replicas identical (the EMA statistics; after the forward-only call the loss slots hold each rank's
+        # local commitment loss, as vqvaes[l].losses does in the reference)
+        nst = 2 * K * D + K
+        assert torch.equal(r0["weights"], r1["weights"]) and torch.equal(r0["stats"][:nst], r1["stats"][:nst])
         for a, b in zip(r0["vq"], r1["vq"]):
             assert all(torch.equal(a[k], b[k]) for k in ("embeddings", "m_t", "N_t")) and a["calls"] == b["calls"]
         # vs one process on the global batch

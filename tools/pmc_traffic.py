@@ -2,11 +2,14 @@
 
     rocprofv3 --pmc FETCH_SIZE --output-format csv -d DIR_F -o f -- python bench.py --no-graph --no-roofline ...
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d DIR_W -o w -- python bench.py --no-graph --no-roofline ...
-    python tools/pmc_traffic.py DIR_F DIR_W profiles/pmc_traffic.json
+    rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d DIR_M -o m -- python bench.py ...
+    python tools/pmc_traffic.py DIR_F DIR_W profiles/pmc_traffic.json [DIR_M]
 
 FETCH_SIZE and WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane streaming
 reads (MI355X_MICROARCH.md § HBM), so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024. Both passes must
 run the same workload; the per-launch figure is the mean over every dispatch of the kernel family.
+MFMA busy fraction (optional third pass) = sum SQ_VALU_MFMA_BUSY_CYCLES / sum (GRBM_GUI_ACTIVE / 8 * 1024):
+GRBM_GUI_ACTIVE is summed over the 8 XCDs, the busy cycles over the 1024 SIMDs (MI355X_MICROARCH.md).
 """
 import csv
 import glob
@@ -47,6 +50,12 @@ def main():
            "per_launch_bytes": int(2 * f_kib * 1024 + w_kib * 1024),
            "note": "bytes = 2 x FETCH_SIZE (gfx950 half-count of 16-B streaming reads) + WRITE_SIZE, "
                    "mean over all dispatches of the kernel family in a --no-graph bench run"}
+    if len(sys.argv) > 4:
+        busy = per_dispatch(sys.argv[4], "SQ_VALU_MFMA_BUSY_CYCLES")
+        grbm = per_dispatch(sys.argv[4], "GRBM_GUI_ACTIVE")
+        if busy and grbm:
+            res["mfma_busy_frac"] = round(sum(busy) / (sum(grbm) / 8 * 1024), 4)
+            res["mfma_dispatches"] = len(busy)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 

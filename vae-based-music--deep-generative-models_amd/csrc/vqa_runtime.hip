@@ -7,6 +7,7 @@
 #include "vqa_common.h"
 #include <stdarg.h>
 #include <stdio.h>
+#include <algorithm>
 
 namespace vqa {
 
@@ -96,6 +97,34 @@ __global__ void step_metrics_kernel(const float* loss_slots, const float* vqm, f
   }
 }
 
+// ---- on-device synthetic waveform feed (replaces the host-side chunk feed of
+// data_utils.py:65-206 splitsongs / read_data and the notebook's tf.data pipeline) --------------------------
+// x[b][t] = clip(0.5 sin(2 pi f_b t / sr + phi_b) + 0.05 eps, -1, 1), f_b ~ U[55, 2000) Hz, phi_b ~ U[0, 2 pi),
+// eps ~ N(0, 1): every draw is a counter-based hash of (seed, rank, item, sample) — no state, any launch
+// shape gives the same batch, ranks draw disjoint streams. The phase is reduced in fp64 (t up to 2^31).
+__device__ __forceinline__ float u01(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }  // [0, 1)
+__device__ __forceinline__ uint64_t feed_key(uint64_t seed, int rank, long long item) {
+  return splitmix64(splitmix64(seed ^ 0x5DEECE66DULL) + ((uint64_t)(unsigned)rank << 40) + (uint64_t)item);
+}
+__global__ __launch_bounds__(256) void synth_kernel(float* x, int B, long long T, uint64_t seed, int rank,
+                                                   double inv_sr) {
+  const int b = blockIdx.y;
+  const uint64_t key = feed_key(seed, rank, b);
+  const double f = 55.0 + (2000.0 - 55.0) * (double)u01(splitmix64(key ^ 1));
+  const float ph = 6.2831853071795864f * u01(splitmix64(key ^ 2));
+  const double cyc_per_sample = f * inv_sr;
+  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < T; t += (long long)gridDim.x * 256) {
+    double c = cyc_per_sample * (double)t;
+    c -= floor(c);
+    const float s = sinf(6.2831853071795864f * (float)c + ph);
+    // Box-Muller from two independent hashes of (key, t)
+    const uint64_t h = splitmix64(key + 0x9E3779B97F4A7C15ULL * (uint64_t)(t + 1));
+    const float u1 = fmaxf(u01(h), 1.0f / 16777216.0f), u2 = u01(splitmix64(h));
+    const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+    x[(long long)b * T + t] = fminf(fmaxf(0.5f * s + 0.05f * eps, -1.0f), 1.0f);
+  }
+}
+
 static int blocks_for(long long n, int cap) {
   long long b = (n + 255) / 256;
   if (b > cap) b = cap;
@@ -150,5 +179,15 @@ extern "C" int vqa_step_metrics(const float* loss_slots, const float* vq_metrics
   hipLaunchKernelGGL(step_metrics_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, loss_slots, vq_metrics, macc,
                      levels, scale);
   VQA_LAUNCHED("step_metrics_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_synthetic_batch(float* x, int B, int64_t T, uint64_t seed, int rank, float sample_rate,
+                                   vqa_stream_t stream) {
+  VQA_ARG(x && B > 0 && T > 0 && B <= 65535 && sample_rate > 0.f, "synthetic_batch: bad arguments");
+  const unsigned gx = (unsigned)std::min<long long>((T + 255) / 256, 1024);
+  hipLaunchKernelGGL(synth_kernel, dim3(gx, (unsigned)B), dim3(256), 0, (hipStream_t)stream, x, B, (long long)T, seed,
+                     rank, 1.0 / (double)sample_rate);
+  VQA_LAUNCHED("synth_kernel");
   return VQA_OK;
 }

@@ -9,7 +9,8 @@ FFTs with TF framing — no centering, frame t = x[t*hop : t*hop+win] times a pe
 zero-padded at the end to n_fft).
 
 File decoding (librosa / GTZAN, data_utils.py:43-206) is out of scope: the north star trains on
-synthetic chunks; `synthetic_batch` generates them.
+synthetic chunks. `synthetic_batch_device` generates them in HBM with a HIP kernel (the
+device feed); `synthetic_batch` is the numpy restatement the tests and the oracle use.
 """
 from __future__ import annotations
 
@@ -84,3 +85,13 @@ def synthetic_batch(B: int, T: int, sr: int = 44100, seed: int = 1234) -> np.nda
     t = np.arange(T)[None, :]
     x = 0.5 * np.sin(2 * np.pi * f * t / sr + ph) + 0.05 * rng.standard_normal((B, T))
     return np.clip(x, -1.0, 1.0).astype(np.float32)[:, :, None]
+
+
+def synthetic_batch_device(B: int, T: int, seed: int = 1234, rank: int = 0, sr: float = 44100.0,
+                           device="cuda", out: torch.Tensor = None) -> torch.Tensor:
+    """The same distribution generated on the GPU (vqa_synthetic_batch: counter-based draws keyed by seed,
+    rank, item and sample), (B, T, 1) fp32 resident in HBM — the device feed of the train step; no host
+    staging. Deterministic per (seed, rank); ranks draw disjoint streams."""
+    x = out if out is not None else torch.empty(B, T, 1, dtype=torch.float32, device=device)
+    V.synthetic_batch(x, seed, rank, sr)
+    return x

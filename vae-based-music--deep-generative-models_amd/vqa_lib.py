@@ -33,7 +33,7 @@ EXPORTED = [
     "vqa_resblock_supported", "vqa_resblock_fwd", "vqa_resblock_bwd", "vqa_resblock_bwd_workspace",
     "vqa_spectral_target_workspace", "vqa_spectral_target", "vqa_spectral_loss_target_workspace",
     "vqa_spectral_loss_target", "vqa_dtail_supported", "vqa_dtail_workspace", "vqa_dtail_fwd", "vqa_dtail_bwd",
-    "vqa_step_metrics",
+    "vqa_step_metrics", "vqa_synthetic_batch",
 ]
 
 
@@ -78,6 +78,7 @@ _SIGS = {
     "vqa_adam_keras": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P]),
     "vqa_counter_add": (_I, [_P, _L, _P]),
     "vqa_step_metrics": (_I, [_P, _P, _P, _I, _F, _P]),
+    "vqa_synthetic_batch": (_I, [_P, _I, _L, _U, _I, _F, _P]),
     "vqa_conv1d_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
     "vqa_conv1d_transpose_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONVT + [_P, _S, _P, _P]),
     "vqa_reduce_partials": (_I, [_P, _I, _P]),
@@ -385,6 +386,14 @@ def adam_keras(w, g, m, v, step, lr, beta1, beta2, eps, grad_scale):
 def step_metrics(loss_slots, vq_metrics, macc, levels, scale):
     _check(lib().vqa_step_metrics(ptr(loss_slots), ptr(vq_metrics), ptr(macc), levels, scale, stream()),
            "vqa_step_metrics")
+
+
+def synthetic_batch(x, seed, rank=0, sample_rate=44100.0):
+    """x: (B, T) or (B, T, 1) fp32 device tensor, filled in place (vqa_synthetic_batch)."""
+    B, T = x.shape[0], x.numel() // x.shape[0]
+    if x.dtype != torch.float32:
+        raise VQAError("synthetic_batch fills an fp32 tensor")
+    _check(lib().vqa_synthetic_batch(ptr(x), B, T, seed, rank, sample_rate, stream()), "vqa_synthetic_batch")
 
 
 def counter_add(counter, delta=1):
