@@ -161,6 +161,24 @@ template <> __device__ __forceinline__ void pos8<float>(const float* p, bool (&m
   for (int i = 0; i < 8; ++i) m[i] = p[i] > 0.f;
 }
 
+// bf16 epilogue helpers on packed bits (two bf16 per dword, packed integer ops: one instruction per pair)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
+// the 8 channels rounded to bf16 (v_cvt_pk_bf16_f32), as raw bits
+__device__ __forceinline__ uint4 bf16_bits(f32x4 lo, f32x4 hi) {
+  const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3], (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+  return __builtin_bit_cast(uint4, o);
+}
+// d * (r > 0) per bf16 where r >= 0 (a relu'd tensor): d's bits times min(r's bits, 1) (v_pk_min_u16 + v_pk_mul_lo_u16)
+__device__ __forceinline__ unsigned mask_pos_pk(unsigned d, unsigned r) {
+  const u16x2 one = {1, 1};
+  const u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(u16x2, r), one);
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(u16x2, d) * m);
+}
+__device__ __forceinline__ uint4 mask_pos8(uint4 d, uint4 r) {
+  return uint4{mask_pos_pk(d.x, r.x), mask_pos_pk(d.y, r.y), mask_pos_pk(d.z, r.z), mask_pos_pk(d.w, r.w)};
+}
+
 // weights -> LDS image [3][32][WS] of A operands: image row k*32 + rs_arow(oc) holds the weights of the
 // conv's output channel oc over its input channels (natural order). TRANSPOSE=true: a forward conv
 // (output = Keras o, input = c); false: the transposed conv (output = c, input = o).
@@ -384,22 +402,29 @@ void resblock_fwd_kernel(ResArgs a) {
         if (wave + 4 * j >= HR / 16) continue;
         const int i = rb[j] + pn, r = t0 - 1 + i;
         const bool live = interior || (r >= 0 && r < a.T);
-        f32x4 v[2];
+        if constexpr (sizeof(T) == 2) {
+          // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8
+          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
+                                                                                            acc[j][1] + bav[1]))));
+          if (!interior && !live) u = uint4{0u, 0u, 0u, 0u};
+          *(uint4*)(H + i * XS + oc) = u;
+          // the tile's own rows 1..RT (rows >= T dropped by the range check)
+          if (a.h && i >= 1 && i <= RT)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, u),
+                                                   rs_rsrc((T*)a.h + (size_t)n * a.T * RC, ibytes),
+                                                   (r * RC + oc) * (int)sizeof(T), 0, 0);
+        } else {
+          f32x4 v[2];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          v[mt] = acc[j][mt] + bav[mt];
-          if (interior) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[mt][q] = fmaxf(v[mt][q], 0.f);
-          } else {
+          for (int mt = 0; mt < 2; ++mt) {
+            v[mt] = acc[j][mt] + bav[mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
+          st8(H + i * XS + oc, v[0], v[1]);
+          if (a.h && i >= 1 && i <= RT)
+            st8_buf<T>(rs_rsrc((T*)a.h + (size_t)n * a.T * RC, ibytes), (r * RC + oc) * (int)sizeof(T), v[0], v[1]);
         }
-        st8(H + i * XS + oc, v[0], v[1]);
-        // the tile's own rows 1..RT (rows >= T dropped by the range check)
-        if (a.h && i >= 1 && i <= RT)
-          st8_buf<T>(rs_rsrc((T*)a.h + (size_t)n * a.T * RC, ibytes), (r * RC + oc) * (int)sizeof(T), v[0], v[1]);
       }
     }
     __syncthreads();  // H complete; every read of X for this tile is done
@@ -497,19 +522,22 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
         if (wave + 4 * j >= nht) continue;
         const int i = rh[j] + pn, r = t0 - d + i;
         const bool live = interior || (r >= 0 && r < a.T);
-        f32x4 v[2];
+        if constexpr (sizeof(T) == 2) {
+          // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8
+          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
+                                                                                            acc[j][1] + bav[1]))));
+          if (!interior && !live) u = uint4{0u, 0u, 0u, 0u};
+          *(uint4*)(H + i * XS + oc) = u;
+        } else {
+          f32x4 v[2];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          v[mt] = acc[j][mt] + bav[mt];
-          if (interior) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[mt][q] = fmaxf(v[mt][q], 0.f);
-          } else {
+          for (int mt = 0; mt < 2; ++mt) {
+            v[mt] = acc[j][mt] + bav[mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
+          st8(H + i * XS + oc, v[0], v[1]);
         }
-        st8(H + i * XS + oc, v[0], v[1]);
       }
     }
     __syncthreads();
@@ -528,6 +556,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     }
     // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
     f32x4 dh[3][2];
+    uint4 dhb[3];  // bf16: the masked dh tile as raw bits (mask applied on the rounded values: same result)
     if (!(a.skip & 4)) {
       int rb[3];
 #pragma unroll
@@ -535,12 +564,16 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       conv_multi<T, false, true, true, 3>(dh, img_frag(wbT), Y, rb, -1);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        bool hp[8];
-        pos8(H + (rh[j] + pn) * XS + oc, hp);
+        if constexpr (sizeof(T) == 2) {
+          dhb[j] = mask_pos8(bf16_bits(dh[j][0], dh[j][1]), *(const uint4*)(H + (rh[j] + pn) * XS + oc));
+        } else {
+          bool hp[8];
+          pos8(H + (rh[j] + pn) * XS + oc, hp);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dh[j][0][q] = hp[q] ? dh[j][0][q] : 0.f;
-          dh[j][1][q] = hp[4 + q] ? dh[j][1][q] : 0.f;
+          for (int q = 0; q < 4; ++q) {
+            dh[j][0][q] = hp[q] ? dh[j][0][q] : 0.f;
+            dh[j][1][q] = hp[4 + q] ? dh[j][1][q] : 0.f;
+          }
         }
       }
     }
@@ -549,7 +582,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= nht) continue;
-        st8(H + (rh[j] + pn) * XS + oc, dh[j][0], dh[j][1]);
+        if constexpr (sizeof(T) == 2) *(uint4*)(H + (rh[j] + pn) * XS + oc) = dhb[j];
+        else st8(H + (rh[j] + pn) * XS + oc, dh[j][0], dh[j][1]);
       }
     }
     __syncthreads();
