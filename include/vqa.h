@@ -196,6 +196,26 @@ int vqa_vq_ema_apply(float* E, float* ET, float* m_t, float* N_t, const float* m
  * bijection on [0, M) with cycle walking. Returns the k-th sampled row of the tiled batch. */
 int64_t vqa_reset_perm_index(uint64_t seed, int64_t counter, int level, int64_t M, int64_t k);
 
+/* ---- upper-level conditioner (src/conditioner/conditioners.py:42-72 ConditionerNet) ---------------
+ * Embedding (layers.Embedding(bins, width), :64): out[n][:] = table[idx[n]][:] (table (K, D) fp32, out in the
+ * activation dtype; an index outside [0, K) gives a zero row). Backward: dtable[k][:] += sum_{n: idx[n]=k}
+ * dy[n][:] in a fixed order (the counting sort + segment sums of the EMA statistics; deterministic). */
+int vqa_embedding_fwd(const float* table, const int64_t* idx, void* out, int64_t N, int D, int K, int dtype,
+                      vqa_stream_t stream);
+int vqa_embedding_bwd(const void* dy, const int64_t* idx, float* dtable, int64_t N, int D, int K, int dtype,
+                      void* workspace, size_t ws_bytes, vqa_stream_t stream);
+size_t vqa_embedding_bwd_workspace(int64_t N, int D, int K);
+/* LayerNormalization(axis=-1, epsilon) (:70): y = (x - mean) / sqrt(var + eps) * gamma + beta over the last
+ * axis (C <= 1024), biased variance, fp32 statistics; x, y in the activation dtype. Backward: dx, and
+ * dgamma = sum dy*xhat, dbeta = sum dy written (per-workgroup partials reduced in a fixed order; desc != NULL
+ * defers that reduction as in the *_partials calls). */
+int vqa_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, int64_t rows, int C, float eps,
+                      int dtype, vqa_stream_t stream);
+int vqa_layernorm_bwd(const void* x, const void* dy, const float* gamma, void* dx, float* dgamma, float* dbeta,
+                      int64_t rows, int C, float eps, int dtype, void* workspace, size_t ws_bytes,
+                      vqa_partials_desc* desc, vqa_stream_t stream);
+size_t vqa_layernorm_bwd_workspace(int64_t rows, int C);
+
 /* ---- losses / optimizer ------------------------------------------------------------------------ */
 /* loss_out[0] = mean((r - x)^2) (vqvae.py:91,125); dr = 2*(r - x)/n + extra (extra nullable). fp32. */
 int vqa_mse_loss(const float* x, const float* r, const float* extra_grad, float* dr, float* loss_out,

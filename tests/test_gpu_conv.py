@@ -49,6 +49,8 @@ CONV_CASES = [
     (64, 1, 2, 1, 1, 2, 513),      # even kernel: SAME pads (0, 1)
     (8, 32, 3, 1, 3, 2, 256),      # generic small widths
     (32, 8, 3, 1, 1, 2, 256),
+    (128, 32, 3, 1, 1, 2, 64),     # ConditionerNet pre conv (embed width 128 -> residual width 32)
+    (32, 128, 3, 1, 1, 2, 300),    # 128-channel output
 ]
 
 
@@ -153,6 +155,7 @@ CONVT_CASES = [
     (32, 32, 1, 37),
     (32, 8, 2, 128),    # generic path
     (64, 32, 2, 256),
+    (32, 128, 2, 64),   # ConditionerNet last up conv (residual width 32 -> embed width 128)
 ]
 
 

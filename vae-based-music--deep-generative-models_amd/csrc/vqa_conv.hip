@@ -1110,6 +1110,7 @@ __global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
   const int tbeg = ch * a.CH, tend = min(a.T_out, tbeg + a.CH);
   const int rows_in = (TT - 1) * a.S + (a.K - 1) * a.D + 1;
   const int E = a.K * a.C * a.O;
+  const int e0 = blockIdx.z * EPT * 256;  // this slice's weight elements [e0, e0 + 4096) (gridDim.z slices)
   const bool relu = a.flags & VQA_PRE_RELU;
   float acc[EPT];
 #pragma unroll
@@ -1128,15 +1129,17 @@ __global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
       xl[e] = relu ? fmaxf(v, 0.f) : v;
     }
     __syncthreads();
-    if (a.flags & WG_DB_FROM_X) {
-      if (threadIdx.x < a.C)
-        for (int r = a.P; r < a.P + nrows * a.S; ++r) dbacc += xl[r * a.C + threadIdx.x];
-    } else if (threadIdx.x < a.O) {
-      for (int r = 0; r < nrows; ++r) dbacc += gl[r * a.O + threadIdx.x];
+    if (blockIdx.z == 0) {
+      if (a.flags & WG_DB_FROM_X) {
+        if (threadIdx.x < a.C)
+          for (int r = a.P; r < a.P + nrows * a.S; ++r) dbacc += xl[r * a.C + threadIdx.x];
+      } else if (threadIdx.x < a.O) {
+        for (int r = 0; r < nrows; ++r) dbacc += gl[r * a.O + threadIdx.x];
+      }
     }
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
-      const int e = threadIdx.x + i * 256;
+      const int e = e0 + threadIdx.x + i * 256;
       if (e < E) {
         const int o = e % a.O, c = (e / a.O) % a.C, k = e / (a.O * a.C);
         float s = acc[i];
@@ -1149,10 +1152,10 @@ __global__ __launch_bounds__(256) void wgrad_direct_kernel(WgradArgs a) {
   float* out = a.ws + (size_t)(n * a.nchunk + ch) * (size_t)(E + a.nb);
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
-    const int e = threadIdx.x + i * 256;
+    const int e = e0 + threadIdx.x + i * 256;
     if (e < E) out[e] = acc[i];
   }
-  if (threadIdx.x < a.nb) out[E + threadIdx.x] = dbacc;
+  if (blockIdx.z == 0 && threadIdx.x < a.nb) out[E + threadIdx.x] = dbacc;
 }
 
 // out1[e] = sum_p ws[p*E + e] for e < E1, out2[e - E1] likewise for e >= E1. Block = 16 elements x 16 part
@@ -1650,7 +1653,8 @@ static int launch_wgrad_direct(const WgradArgs& a, const WgradPlan& p, hipStream
   static size_t lds_set = 0;
   const int rc = ensure_dyn_lds((const void*)wgrad_direct_kernel<TX, TG, 64>, p.lds, &lds_set, "wgrad_direct_kernel");
   if (rc != VQA_OK) return rc;
-  hipLaunchKernelGGL((wgrad_direct_kernel<TX, TG, 64>), dim3(p.nchunk, a.B), dim3(256), p.lds, s, a);
+  const unsigned slices = (unsigned)((a.K * a.C * a.O + 4095) / 4096);  // 16 weight elements per thread per slice
+  hipLaunchKernelGGL((wgrad_direct_kernel<TX, TG, 64>), dim3(p.nchunk, a.B, slices), dim3(256), p.lds, s, a);
   VQA_LAUNCHED("wgrad_direct_kernel");
   return VQA_OK;
 }
@@ -1682,8 +1686,8 @@ int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_i
   WgradPlan p = plan_wgrad(dtype, B, T_in, T_out, C, O, K, S, D, flags);
   VQA_ARG(ws && ws_bytes >= p.ws_bytes, "workspace too small: need %zu bytes, got %zu", p.ws_bytes, ws_bytes);
   VQA_REQUIRE(p.lds <= 150 * 1024, VQA_E_UNSUPPORTED, "wgrad: LDS tile too large (%zu B)", p.lds);
-  VQA_REQUIRE(p.kind != WG_DIRECT || K * C * O <= 16 * 256, VQA_E_UNSUPPORTED,
-              "wgrad: generic path limited to K*C*O<=4096");
+  VQA_REQUIRE(p.kind != WG_DIRECT || K * C * O <= 16 * 256 * 64, VQA_E_UNSUPPORTED,
+              "wgrad: generic path limited to K*C*O<=262144");
   VQA_REQUIRE(p.nb <= 256 && 256 % p.nb == 0, VQA_E_UNSUPPORTED, "wgrad: bias width must divide 256");
   WgradArgs a{x, g, (float*)ws, B, T_in, T_out, C, O, K, S, D, P, p.CH, p.nchunk, flags, p.nb};
   const bool xf = dtype == VQA_F32 || (flags & VQA_X_F32);

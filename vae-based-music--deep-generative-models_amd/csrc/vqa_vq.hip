@@ -494,7 +494,8 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t
   extern __shared__ int hist[];  // [K]
   __shared__ __attribute__((aligned(16))) int codes[kSortChunk];
   const int c = blockIdx.x, tid = threadIdx.x, row = c * kSortChunk + tid;
-  const int k = row < N ? (int)idx[row] : -1;
+  const int64_t v = row < N ? idx[row] : -1;
+  const int k = (v >= 0 && v < K) ? (int)v : -1;  // an index outside [0, K) contributes to no code
   codes[tid] = k;
   for (int i = tid; i < K; i += kSortChunk) hist[i] = 0;
   __syncthreads();
@@ -505,7 +506,7 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t
     const int4 q = *(const int4*)(codes + j);
     r += (q.x == k && j < tid) + (q.y == k && j + 1 < tid) + (q.z == k && j + 2 < tid) + (q.w == k && j + 3 < tid);
   }
-  if (row < N) {
+  if (k >= 0) {
     w.lrank[row] = r;
     atomicAdd(hist + k, 1);  // integer: order-independent
   }
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(1024) void vq_sort_scan_kernel(SortWs w, float* n_s
     }
     if (k < K) {
       w.tot[k] = run;
-      n_sum[k] += (float)run;
+      if (n_sum) n_sum[k] += (float)run;
     }
   }
   __syncthreads();
@@ -580,17 +581,20 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_scatter_kernel(const int64
   if (c == 0)
     for (int i = threadIdx.x; i <= K; i += kSortChunk) w.seg[i] = seg[i];
   if (row >= N) return;
-  const int k = (int)idx[row];
+  const int64_t v = idx[row];
+  if (v < 0 || v >= K) return;
+  const int k = (int)v;
   const int pos = seg[k] + w.cnt[(size_t)c * K + k] + w.lrank[row];
   w.perm[pos] = row;
   w.scode[pos] = k;
 }
 
 template <class T>
-__global__ __launch_bounds__(256) void vq_seg_sum_kernel(const T* z, SortWs w, float* m_sumT, int N, int D) {
+__global__ __launch_bounds__(256) void vq_seg_sum_kernel(const T* z, SortWs w, float* m_sumT, int K, int D) {
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int p0 = tile * kSegTile;
+  const int N = w.seg[K];  // sorted positions = rows with a valid code
   if (p0 >= N) return;
   const int np = min(kSegTile, N - p0);
   const int myrow = lane < np ? w.perm[p0 + lane] : 0;
@@ -662,7 +666,7 @@ static int launch_ema_sums(const T* z, const int64_t* idx, float* m_sumT, float*
   VQA_LAUNCHED("vq_sort_scan_kernel");
   hipLaunchKernelGGL(vq_sort_scatter_kernel, dim3(nch), dim3(kSortChunk), (size_t)(K + 1) * 4, s, idx, w, (int)N, K);
   VQA_LAUNCHED("vq_sort_scatter_kernel");
-  hipLaunchKernelGGL(vq_seg_sum_kernel<T>, dim3((ntile + 3) / 4), dim3(256), 0, s, z, w, m_sumT, (int)N, D);
+  hipLaunchKernelGGL(vq_seg_sum_kernel<T>, dim3((ntile + 3) / 4), dim3(256), 0, s, z, w, m_sumT, K, D);
   VQA_LAUNCHED("vq_seg_sum_kernel");
   hipLaunchKernelGGL(vq_seg_combine_kernel, dim3(K), dim3(256), 0, s, w, m_sumT, D);
   VQA_LAUNCHED("vq_seg_combine_kernel");
@@ -842,4 +846,18 @@ extern "C" int vqa_vq_ema_apply(float* E, float* ET, float* m_t, float* N_t, con
 extern "C" int64_t vqa_reset_perm_index(uint64_t seed, int64_t counter, int level, int64_t M, int64_t k) {
   if (M <= 0 || k < 0 || k >= M) return -1;
   return perm_index(perm_key(seed, counter, level), M, k);
+}
+
+extern "C" size_t vqa_embedding_bwd_workspace(int64_t N, int D, int K) { return sort_ws_bytes(N, D, K); }
+
+extern "C" int vqa_embedding_bwd(const void* dy, const int64_t* idx, float* dtable, int64_t N, int D, int K, int dtype,
+                                 void* workspace, size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(dy && idx && dtable && N > 0 && D > 0 && K > 0, "embedding_bwd: bad arguments");
+  VQA_ARG(N < (1ll << 31) - kSortChunk && D <= 1024 && K <= kMaxSortK, "embedding_bwd: N=%lld D=%d K=%d out of range",
+          (long long)N, D, K);
+  VQA_ARG(dtype == VQA_BF16 || dtype == VQA_F32, "embedding_bwd: unknown dtype %d", dtype);
+  VQA_ARG(workspace && ws_bytes >= sort_ws_bytes(N, D, K), "embedding_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == VQA_BF16 ? launch_ema_sums<bf16>((const bf16*)dy, idx, dtable, nullptr, N, D, K, workspace, s)
+                           : launch_ema_sums<float>((const float*)dy, idx, dtable, nullptr, N, D, K, workspace, s);
 }

@@ -40,7 +40,8 @@ class ParamStore:
         return name
 
     def init_values(self, seed: int = 1) -> Dict[str, np.ndarray]:
-        """keras defaults: glorot_uniform kernels, zero biases (numpy, registration order)."""
+        """keras defaults (numpy, registration order): glorot_uniform conv kernels, zero biases; Embedding
+        'uniform' = U(-0.05, 0.05); LayerNormalization gamma 'ones', beta zeros."""
         rng = np.random.default_rng(seed)
         vals = {}
         for name, shape, init in self.specs:
@@ -48,6 +49,10 @@ class ParamStore:
                 K = shape[0]
                 lim = math.sqrt(6.0 / (K * shape[1] + K * shape[2]))
                 vals[name] = rng.uniform(-lim, lim, size=shape).astype(np.float32)
+            elif init == "uniform":
+                vals[name] = rng.uniform(-0.05, 0.05, size=shape).astype(np.float32)
+            elif init == "ones":
+                vals[name] = np.ones(shape, np.float32)
             else:
                 vals[name] = np.zeros(shape, np.float32)
         return vals

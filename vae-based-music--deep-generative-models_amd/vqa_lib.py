@@ -34,6 +34,8 @@ EXPORTED = [
     "vqa_spectral_target_workspace", "vqa_spectral_target", "vqa_spectral_loss_target_workspace",
     "vqa_spectral_loss_target", "vqa_dtail_supported", "vqa_dtail_workspace", "vqa_dtail_fwd", "vqa_dtail_bwd",
     "vqa_step_metrics", "vqa_synthetic_batch",
+    "vqa_embedding_fwd", "vqa_embedding_bwd", "vqa_embedding_bwd_workspace", "vqa_layernorm_fwd",
+    "vqa_layernorm_bwd", "vqa_layernorm_bwd_workspace",
 ]
 
 
@@ -79,6 +81,12 @@ _SIGS = {
     "vqa_counter_add": (_I, [_P, _L, _P]),
     "vqa_step_metrics": (_I, [_P, _P, _P, _I, _F, _P]),
     "vqa_synthetic_batch": (_I, [_P, _I, _L, _U, _I, _F, _P]),
+    "vqa_embedding_fwd": (_I, [_P, _P, _P, _L, _I, _I, _I, _P]),
+    "vqa_embedding_bwd": (_I, [_P, _P, _P, _L, _I, _I, _I, _P, _S, _P]),
+    "vqa_embedding_bwd_workspace": (_S, [_L, _I, _I]),
+    "vqa_layernorm_fwd": (_I, [_P, _P, _P, _P, _L, _I, _F, _I, _P]),
+    "vqa_layernorm_bwd": (_I, [_P, _P, _P, _P, _P, _P, _L, _I, _F, _I, _P, _S, _P, _P]),
+    "vqa_layernorm_bwd_workspace": (_S, [_L, _I]),
     "vqa_conv1d_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONV + [_P, _S, _P, _P]),
     "vqa_conv1d_transpose_bwd_weight_partials": (_I, [_P, _P, _P, _P] + _CONVT + [_P, _S, _P, _P]),
     "vqa_reduce_partials": (_I, [_P, _I, _P]),
@@ -394,6 +402,43 @@ def synthetic_batch(x, seed, rank=0, sample_rate=44100.0):
     if x.dtype != torch.float32:
         raise VQAError("synthetic_batch fills an fp32 tensor")
     _check(lib().vqa_synthetic_batch(ptr(x), B, T, seed, rank, sample_rate, stream()), "vqa_synthetic_batch")
+
+
+def embedding_fwd(table, idx, out):
+    """src/conditioner/conditioners.py:64 layers.Embedding: out (..., D) = table[idx] (vqa_embedding_fwd)."""
+    K, D = table.shape
+    N = idx.numel()
+    if idx.dtype != torch.int64 or out.shape[-1] != D or out.numel() != N * D:
+        raise VQAError("embedding_fwd: idx int64 (...), out (..., D)")
+    _check(lib().vqa_embedding_fwd(ptr(table), ptr(idx), ptr(out), N, D, K, dtype_code(out.dtype), stream()),
+           "vqa_embedding_fwd")
+
+
+def embedding_bwd(dy, idx, dtable):
+    """dtable[k] += sum of dy rows with idx == k, fixed order (vqa_embedding_bwd)."""
+    K, D = dtable.shape
+    N = idx.numel()
+    ws = workspace(lib().vqa_embedding_bwd_workspace(N, D, K), dy.device)
+    _check(lib().vqa_embedding_bwd(ptr(dy), ptr(idx), ptr(dtable), N, D, K, dtype_code(dy.dtype), ptr(ws), ws.numel(),
+                                   stream()), "vqa_embedding_bwd")
+
+
+def layernorm_fwd(x, gamma, beta, y, eps):
+    C = x.shape[-1]
+    _check(lib().vqa_layernorm_fwd(ptr(x), ptr(gamma), ptr(beta), ptr(y), x.numel() // C, C, eps, dtype_code(x.dtype),
+                                   stream()), "vqa_layernorm_fwd")
+
+
+def layernorm_bwd(x, dy, gamma, dx, dgamma, dbeta, eps, deferred=None):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    ws = workspace(lib().vqa_layernorm_bwd_workspace(rows, C), x.device)
+    d = PartialsDesc() if deferred is not None else None
+    _check(lib().vqa_layernorm_bwd(ptr(x), ptr(dy), ptr(gamma), ptr(dx), ptr(dgamma), ptr(dbeta), rows, C, eps,
+                                   dtype_code(x.dtype), ptr(ws), ws.numel(), ctypes.byref(d) if d is not None else None,
+                                   stream()), "vqa_layernorm_bwd")
+    if deferred is not None:
+        deferred.add(d, ws)
 
 
 def counter_add(counter, delta=1):
