@@ -1180,6 +1180,33 @@ __device__ __forceinline__ float reduce_col16(const float* ws, int nparts, int E
   return t;
 }
 
+// 16-byte form for rows whose length and base keep float4 alignment: block = 64 elements (16 lanes x 4) x 16
+// part groups, so each wave reads 256 contiguous bytes of 4 rows per load. Fixed order as above.
+constexpr int kRedCols4 = 64;
+__device__ __forceinline__ f32x4 reduce_col64(const float* ws, int nparts, int E, int e, f32x4 (*red)[16]) {
+  const int el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  f32x4 s[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (e < E) {
+    int p = grp;
+    for (; p + 7 * 16 < nparts; p += 8 * 16)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += *(const f32x4*)(ws + (size_t)(p + 16 * u) * E + e);
+    for (; p < nparts; p += 16) s[0] += *(const f32x4*)(ws + (size_t)p * E + e);
+  }
+  red[grp][el] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  f32x4 t = {0.f, 0.f, 0.f, 0.f};
+  if (grp == 0)
+    for (int g = 0; g < 16; ++g) t += red[g][el];
+  return t;
+}
+
+static bool desc_vec4(const vqa_partials_desc& d) {
+  return d.n % 4 == 0 && ((uintptr_t)d.partials & 15) == 0;
+}
+
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* ws, int nparts, int E, int E1,
                                                              float* out1, float* out2) {
   __shared__ float red[16][kRedCols];
@@ -1200,14 +1227,32 @@ constexpr int kMaxDescs = 48;
 struct ReduceBatch {
   vqa_partials_desc d[kMaxDescs];
   int start[kMaxDescs + 1];
+  int vec4[kMaxDescs];
   int count;
 };
 
 __global__ __launch_bounds__(256) void reduce_partials_batched_kernel(ReduceBatch rb) {
-  __shared__ float red[16][kRedCols];
+  __shared__ f32x4 red4[16][16];
   int i = 0;
   while (i + 1 < rb.count && (int)blockIdx.x >= rb.start[i + 1]) ++i;
   const vqa_partials_desc& d = rb.d[i];
+  if (rb.vec4[i]) {
+    const int e = ((int)blockIdx.x - rb.start[i]) * kRedCols4 + 4 * (threadIdx.x & 15);
+    const f32x4 s = reduce_col64(d.partials, d.nparts, d.n, e, red4);
+    if (threadIdx.x < 16 && e < d.n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int eq = e + q;
+        if (eq < d.n_w) {
+          if (d.dw) d.dw[eq] = s[q];
+        } else if (d.db) {
+          d.db[eq - d.n_w] = s[q];
+        }
+      }
+    }
+    return;
+  }
+  float(*red)[kRedCols] = (float(*)[kRedCols])red4;
   const int e = ((int)blockIdx.x - rb.start[i]) * kRedCols + (threadIdx.x & (kRedCols - 1));
   const float s = reduce_col16(d.partials, d.nparts, d.n, e, red);
   if (threadIdx.x < kRedCols && e < d.n) {
@@ -1967,7 +2012,8 @@ extern "C" int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vq
       VQA_ARG(d.partials && d.n > 0 && d.nparts > 0 && d.n_w <= d.n, "reduce_partials: bad descriptor %d", base + i);
       rb.d[i] = d;
       rb.start[i] = blocks;
-      blocks += (d.n + kRedCols - 1) / kRedCols;
+      rb.vec4[i] = desc_vec4(d) ? 1 : 0;
+      blocks += rb.vec4[i] ? (d.n + kRedCols4 - 1) / kRedCols4 : (d.n + kRedCols - 1) / kRedCols;
     }
     rb.start[rb.count] = blocks;
     hipLaunchKernelGGL(reduce_partials_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);

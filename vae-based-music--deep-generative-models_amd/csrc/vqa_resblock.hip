@@ -458,8 +458,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   constexpr int WS = rs_stride<T>(), XS = WS, NT = RT / 16, NJ = (NT + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int d = DT > 0 ? DT : a.d, HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
-  T* waF = (T*)smem;            // conv_a forward (recompute h): output o, input c
-  T* waT = waF + 3 * RC * WS;   // conv_a^T: output c, input o
+  // conv_a's forward A fragments (recompute h) live in registers; the two transposed convs read LDS images
+  T* waT = (T*)smem;            // conv_a^T: output c, input o
   T* wbT = waT + 3 * RC * WS;   // conv_b^T: output c, input o
   T* X = wbT + 3 * RC * WS;     // local j <-> row t0 - 2d + j: relu(x)
   T* Y = X + XR * XS;           // local m <-> row t0 - d - 1 + m (dy)
@@ -468,7 +468,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
             tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
-  stage_wimg<T, true>(waF, a.wa);
+  typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()];
+  load_wfrags<T, true>(wfa, a.wa);
   stage_wimg<T, false>(waT, a.wa);
   stage_wimg<T, false>(wbT, a.wb);
   const int pn = rs_pi(lane & 15), oc = rs_ocol(lane), kc = rs_kcol<T, true>(lane);
@@ -516,7 +517,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     for (int j = 0; j < 3; ++j) rh[j] = min(wave + 4 * j, nht - 1) * 16;
     if (!(a.skip & 1)) {
       f32x4 acc[3][2];
-      conv_multi<T, false, true, true, 3>(acc, img_frag(waF), X, rh, d);
+      auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
+      conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= nht) continue;
@@ -661,6 +663,7 @@ static int rs_cus() {
   return n;
 }
 constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the partial rows)
+constexpr int kResMinTiles = 4;  // backward: tiles per workgroup at least (bounds the partial rows of short launches)
 
 static size_t fwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = rt + 16;
@@ -668,7 +671,7 @@ static size_t fwd_lds(int d, int esz, int rt) {
 }
 static size_t bwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = round16(rt + 2 * d);
-  return ((size_t)9 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
+  return ((size_t)6 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
 }
 
 static int set_lds(const void* fn, size_t bytes) {
@@ -709,12 +712,12 @@ template <class F> static const void* rs_pick(int d) {
 static int fwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_fwd_rt(d) : RTM; }
 static int bwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_bwd_rt(d) : RTM; }
 
-static void plan(ResArgs& a, int per_cu, int rt) {
+static void plan(ResArgs& a, int per_cu, int rt, int min_tiles = 1) {
   a.ntm = (a.T + rt - 1) / rt;
   a.ntiles = a.ntm * a.B;
   // every slot gets floor(ntiles / nwg) tiles and the first (ntiles mod nwg) one more: workgroups w and
   // w + #CUs (dispatched to the same CU) never both hold an extra tile while extras <= #CUs
-  a.nwg = std::min(rs_cus() * per_cu, a.ntiles);
+  a.nwg = std::min(rs_cus() * per_cu, std::max(1, a.ntiles / min_tiles));
   a.tpw = a.ntiles / a.nwg;
   a.textra = a.ntiles - a.tpw * a.nwg;
 }
@@ -781,7 +784,9 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   }();
   a.skip = dbg_skip;
 #endif
-  plan(a, kResPerCU, bwd_rt_of(dilation));
+  // at least kResMinTiles tiles per workgroup: a workgroup's weight-gradient partial row (2 x 3,104 fp32) is
+  // larger than a tile's activations, so short launches use fewer, longer-lived workgroups
+  plan(a, kResPerCU, bwd_rt_of(dilation), kResMinTiles);
   const int nwg = a.nwg;
   a.part_b = a.part_a + (size_t)nwg * E;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
