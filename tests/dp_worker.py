@@ -42,6 +42,7 @@ def snapshot(m):
     P = m.layout["grads"][1]
     return {"weights": m.store.flat.detach().cpu().clone(), "adam_m": m.optimizer.m.cpu().clone(),
             "adam_v": m.optimizer.v.cpu().clone(), "stats": m.bucket[P:].detach().cpu().clone(),
+            "grads": m.bucket[:P].detach().cpu().clone(),
             "vq": [{k: torch.as_tensor(v) for k, v in st.items() if k != "calls"} | {"calls": st["calls"]}
                    for st in m.get_vq_state()],
             "results": {k: float(v) for k, v in m.results().items()}}

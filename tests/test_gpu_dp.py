@@ -82,7 +82,14 @@ def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode):
         # the same global rows selected (their values carry step 1's fp32 weight differences)
         assert _rel(RT, ss[K * D + K:2 * K * D + K]) < 1e-5, f"{phase}: reset rows"
         assert _rel(m_sum, ss[:K * D]) < 1e-6, f"{phase}: EMA sums"
-        assert _rel(r0["weights"], s["weights"]) < 1e-6, f"{phase}: weights"
+        if phase == "steps":
+            # the exchanged gradient (sum over ranks of rank-mean gradients) = world x the global-batch mean
+            # gradient, to fp32 rounding of the different summation grouping
+            assert _rel(r0["grads"] / 2, s["grads"]) < 2e-6, f"{phase}: gradients"
+        # Adam normalises each element by sqrt(v): an element whose gradient nearly cancels across items keeps
+        # its absolute rounding noise but has a small sqrt(v), so a 1e-7-relative gradient difference becomes
+        # up to ~1e-3 of that element's update (Keras default lr = 1e-3 per step), i.e. a few 1e-6 of max|w|
+        assert _rel(r0["weights"], s["weights"]) < 1e-5, f"{phase}: weights"
         if phase == "steps":
             assert _rel(r0["adam_m"], s["adam_m"]) < 1e-5 and _rel(r0["adam_v"], s["adam_v"]) < 1e-5
         for a, b in zip(r0["vq"], s["vq"]):
