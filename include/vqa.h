@@ -270,6 +270,94 @@ int vqa_spectral_loss_target(const void* target, const float* r, float* loss_out
 /* data_utils.py:25-30 spectral(x) for one resolution: mag (B, F, n_fft/2 + 1) fp32 = |tf.signal.stft(x)|. */
 int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int n_fft, int hop, int win, vqa_stream_t stream);
 
+/* ==== factorized-attention prior (BASELINE configs 4-5) ==================== *
+ * src/transformer/{factorized_attention,transformer}.py, src/autoregressive/autoregressive_fmha.py, prior.py.
+ * Rows are (nseq, T) sequences of channels-last vectors in the activation dtype; weights fp32, Keras layouts. */
+
+/* Sequence-linear layer (MFMA): y[r][n] = sum_tap sum_k x[src(r,tap)][k] * Wv[tap][k][n] + bias[n]
+ * (+ residual[r][n]) (+ y[r][n] when accumulate), src(r,tap) = the same sequence at t + dir*(taps-1-tap), zero
+ * outside [0, T). Wv[tap][k][n] = wtrans ? w[(tap*N + n)*K + k] : w[(tap*K + k)*N + n].
+ *   dir=-1, taps=3, wtrans=0: Conv1D(3w, 3, padding="causal") (factorized_attention.py:36)
+ *   dir=+1, taps=3, wtrans=1: its data gradient
+ *   taps=1: layers.Dense / MultiHeadAttention EinsumDense (factorized_attention.py:39-50, transformer.py:30)
+ *           and, wtrans=1, their data gradients.
+ * ldx/ldr/ldy are row strides in elements (column slices of a wider tensor are allowed). K <= 256, N <= 128,
+ * N % 16 == 0, K % 32 (bf16) / 4 (fp32) == 0. */
+int vqa_seqlin_fwd(const void* x, int64_t ldx, const float* w, const float* bias, const void* residual, int64_t ldr,
+                   void* y, int64_t ldy, int nseq, int T, int K, int N, int taps, int dir, int wtrans, int accumulate,
+                   int dtype, vqa_stream_t stream);
+/* dW[tap][k][n] = sum_t x[t-(taps-1-tap)][k] dy[t][n], db = sum_t dy[t] (deterministic partials; desc != NULL
+ * defers the reduction as for the conv weight gradients). K <= 128, N <= 128, multiples of 16. */
+size_t vqa_seqlin_wgrad_workspace(int nseq, int T, int K, int N, int taps);
+int vqa_seqlin_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dw, float* db, int nseq, int T,
+                     int K, int N, int taps, int dtype, void* workspace, size_t ws_bytes, vqa_partials_desc* desc,
+                     vqa_stream_t stream);
+/* autoregressive_fmha.py:119-151: out = table[tokens] (row 0 <- ycond when given) * scale + pos[t]; keras
+ * Dropout(rate) with a counter-based mask (seed, and the device step counter when given, so a replayed graph
+ * draws a new mask each step); + xcond (N, T, W) when given. */
+int vqa_prior_embed_fwd(const float* table, const float* pos, const int64_t* tokens, const float* ycond,
+                        const void* xcond, void* out, int N, int T, int W, int bins, float scale, float rate,
+                        uint64_t seed, const int64_t* counter, int dtype, vqa_stream_t stream);
+/* out[i] (+)= sum_{n < nout} x[n*ostride + i], i < inner (fp32 out, fixed order): positional-embedding and
+ * bias gradients. */
+int vqa_colsum(const void* x, float* out, int nout, int64_t ostride, int64_t inner, int accumulate, int dtype,
+               vqa_stream_t stream);
+int vqa_axpy(const void* x, const void* y, void* z, int64_t n, int dtype, vqa_stream_t stream); /* z = x + y */
+/* keras Dropout(rate) in place: x * 1/(1-rate) where uniform(seed, salt, i) >= rate, else 0. */
+int vqa_dropout(void* x, int64_t n, float rate, uint64_t seed, uint64_t salt, const int64_t* counter, int dtype,
+                vqa_stream_t stream);
+int vqa_scale_f32(float* x, int64_t n, float s, vqa_stream_t stream);
+/* prior.py:262-290 teacher forcing: latent = [start, codes[:-1]]; pred = [start, amax[:-1]];
+ * out = m ? pred : latent, m = mask[r] (uint8, when given) or uniform(seed, step + *counter, r) < rate; amax
+ * NULL: out = latent. */
+int vqa_tf_mix(const int64_t* codes, const int64_t* amax, const uint8_t* mask, int64_t* out, int N, int T,
+               int64_t start, float rate, uint64_t seed, uint64_t step, const int64_t* counter, vqa_stream_t stream);
+/* Factorized attention core of keras MultiHeadAttention (softmax(q k^T * scale + mask) v per head) on the
+ * projected q, k, v (N, T, H*head_dim), head_dim 16. mode 0 row (causal within blocks of l,
+ * factorized_attention.py:74-141), 1 col (causal over blocks at a fixed position, :210-286), 2 prev-row
+ * (block b attends block b-1; block 0 attends the zero block, so o = vbias, :308-388). lse (N, T, H) fp32
+ * (log2 domain) is saved for the backward. Modes 0/2 need l % 64 == 0; mode 1 needs T/l <= 8. */
+int vqa_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* vbias, int N, int T,
+                 int H, int head_dim, int l, int mode, float scale, int dtype, vqa_stream_t stream);
+/* dq, dk, dv from dout (deterministic: one kernel per query tile for dq, one per key tile for dk/dv).
+ * dsum: (N, T, H) fp32 scratch (modes 0/2). For mode 2 the zero block's value-bias gradient is the column
+ * sum of dout over block 0 (vqa_colsum); dq of block 0 is zero. */
+int vqa_attn_bwd(const void* q, const void* k, const void* v, const void* o, const float* lse, const void* dout,
+                 float* dsum, void* dq, void* dk, void* dv, int N, int T, int H, int head_dim, int l, int mode,
+                 float scale, int dtype, vqa_stream_t stream);
+/* Output head Dense(bins) fused with SparseCategoricalCrossentropy(from_logits) / accuracy
+ * (autoregressive_fmha.py:80,158; autoregressive.py:189-212); logits are never written. wt = W^T (V, K) in
+ * the activation dtype (vqa_head_wt). K = 128. head_fwd: per row lse, argmax (first maximum), and with
+ * targets the row loss lse - logit[target] and correctness (1/0). head_bwd: dx = dlogits W^T, dW, db with
+ * dlogits = (softmax - onehot) * inv_count. */
+int vqa_head_wt(const float* w, void* wt, int K, int V, int dtype, vqa_stream_t stream);
+int vqa_head_fwd(const void* x, const void* wt, const float* bias, const int64_t* targets, float* lse, int64_t* amax,
+                 float* loss_row, float* correct, int64_t M, int K, int V, int dtype, vqa_stream_t stream);
+size_t vqa_head_bwd_workspace(int64_t M, int K, int V);
+int vqa_head_bwd(const void* x, const void* wt, const float* bias, const int64_t* targets, const float* lse,
+                 float inv_count, void* dx, float* dw, float* db, int64_t M, int K, int V, int dtype, void* workspace,
+                 size_t ws_bytes, vqa_partials_desc* desc, vqa_stream_t stream);
+/* out[i] = scale * sum_j x[i*n + j] (fixed order). */
+int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, float* out, vqa_stream_t stream);
+
+/* Autoregressive sampling (autoregressive_fmha.py:162-240, Sampler.py): one persistent workgroup per sample
+ * walks `steps` positions with a key/value cache, z = logits + Gumbel(uniform(seed, sample, step, bin)),
+ * next token = argmax z. tokens (N, steps+1) int64 with tokens[:, 0] = start. Optional: ycond (N, width)
+ * label embedding for position 0, xcond (N, ctx, width) fp32 upper-level conditioning, forced (N, steps+1)
+ * input tokens (teacher-forced check), logits (N, steps, bins) output. width 128, attention width 32. */
+typedef struct {
+  const float *ln1_gamma, *ln1_beta, *qkv_kernel, *qkv_bias, *query_kernel, *query_bias, *key_kernel, *key_bias,
+      *value_kernel, *value_bias, *out_kernel, *out_bias, *proj_kernel, *proj_bias, *ln2_gamma, *ln2_beta,
+      *mlp_kernel, *mlp_bias;
+  int attn_type; /* 0 row, 1 col, 2 prev-row (transformer.py:82-86) */
+} vqa_prior_layer;
+size_t vqa_prior_decode_cache_bytes(int N, int depth, int ctx);
+int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const float* x_embedding, const float* pos_embedding,
+                     const float* out_kernel, const float* out_bias, const float* ycond, const float* xcond,
+                     const int64_t* forced, float* logits, int64_t* tokens, void* cache, size_t cache_bytes, int N,
+                     int steps, int ctx, int width, int heads, int blocks, int bins, int64_t start, uint64_t seed,
+                     vqa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

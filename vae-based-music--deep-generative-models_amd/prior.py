@@ -1,0 +1,576 @@
+"""Factorized-attention prior — drop-in for the reference's prior stack (BASELINE configs 4-5).
+
+Reference classes kept here (same names, constructor arguments and call surface):
+  src/transformer/factorized_attention.py:10-72  FactorizedAttention(ctc_len, num_heads, d_model, blocks, attn_func,
+                                                   m_attn, drop_out_rate): causal Conv1D(3w, 3) -> split q, k, v ->
+                                                   keras MultiHeadAttention(num_heads, key_dim=w/H) core of the
+                                                   row (0) / col (1) / prev-row (2) factorization -> Dense(d_model)
+  src/transformer/transformer.py:12-60           ResidualAttnBlock: out = mlp(LN2(x + a)) + a + x, a = fmha(LN1(x))
+  src/transformer/transformer.py:63-115          FactorizedTransformer (attn_stacks 0: row/col, 1: row/col/prev-row)
+  src/autoregressive/autoregressive_fmha.py:13-240  FMHABasedAutoregressiveModel: embedding * sqrt(d) + positional
+                                                   embedding (+ x_cond from ConditionerNet), transformer, Dense(bins);
+                                                   sample() = Gumbel-max ancestral sampling
+  prior.py:102-372                               Prior: train_step with teacher forcing (two forward passes, the
+                                                   second mixes the first pass's argmax into the input at
+                                                   teacher_force_rate), loss/accuracy trackers, Keras Adam
+  src/conditioner/label_conditioners.py:9-48     LabelConditioner (genre Embedding -> the start position)
+
+MI355X path (libvqa, vqa_prior.hip): every linear layer is the MFMA sequence-linear kernel (the causal conv is
+its 3-tap form); attention is flash-style on MFMA for the row / prev-row blocks and a register kernel for the
+4-long columns; the output Dense is fused with the cross entropy / argmax so the (N, T, bins) logits are never
+written; sampling is ONE persistent kernel per batch that walks the positions with a key/value cache instead of
+re-running the model on the prefix at every step. All gradients are explicit; weight gradients are fixed-order
+partial reductions (deterministic). Dropout uses a counter-based mask (TF's RNG cannot be replayed).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+import vqa_lib as V
+from conditioners import ConditionerNet
+from vqa_layers import ParamStore
+from vqa_metrics import Mean
+from vqa_optim import Adam
+
+
+def create_look_ahead_mask(q_len, k_len):
+    """multi_head_attention.py:27-30 (1 = attend)."""
+    return torch.tril(torch.ones(q_len, k_len))
+
+
+def positional_encoding(position, d_model):
+    """multi_head_attention.py:33-59: (1, position, d_model) sinusoid table (fp32)."""
+    pos = np.arange(position)[:, None]
+    i = np.arange(d_model)[None, :]
+    ang = pos / np.power(10000, (2 * (i // 2)) / np.float32(d_model))
+    ang[:, 0::2] = np.sin(ang[:, 0::2])
+    ang[:, 1::2] = np.cos(ang[:, 1::2])
+    return ang[None].astype(np.float32)
+
+
+ATTN_NAMES = {0: "row", 1: "col", 2: "prev row"}
+
+
+class FactorizedAttention:
+    def __init__(self, ctc_len, num_heads, d_model, blocks, attn_func=0, m_attn=0.25, drop_out_rate=0.0, **kwargs):
+        self.width = int(d_model * m_attn)
+        assert self.width % num_heads == 0
+        self.num_heads, self.ctx_len, self.blocks, self.d_model = num_heads, ctc_len, blocks, d_model
+        assert self.ctx_len % blocks == 0
+        self.block_len = self.ctx_len // blocks
+        self.attn_func, self.attn_type = attn_func, ATTN_NAMES[attn_func]
+        self.rate = drop_out_rate
+        self.head_dim = self.width // num_heads
+
+    def build(self, store: ParamStore, prefix: str):
+        w, H, hd, d = self.width, self.num_heads, self.head_dim, self.d_model
+        self.prefix, self.store = prefix, store
+        store.add(f"{prefix}/qkv/kernel", (3, d, 3 * w), "glorot_uniform")
+        store.add(f"{prefix}/qkv/bias", (3 * w,), "zeros")
+        for n in ("query", "key", "value"):
+            store.add(f"{prefix}/mha/{n}/kernel", (w, H, hd), "glorot_uniform")
+            store.add(f"{prefix}/mha/{n}/bias", (H, hd), "zeros")
+        store.add(f"{prefix}/mha/out/kernel", (H, hd, w), "glorot_uniform")
+        store.add(f"{prefix}/mha/out/bias", (w,), "zeros")
+        store.add(f"{prefix}/proj/kernel", (w, d), "glorot_uniform")
+        store.add(f"{prefix}/proj/bias", (d,), "zeros")
+
+    def p(self, name):
+        return self.store.view(f"{self.prefix}/{name}")
+
+    def g(self, name):
+        return self.store.grad_view(f"{self.prefix}/{name}")
+
+
+class ResidualAttnBlock:
+    def __init__(self, ctc_len, num_heads, d_model, blocks, attn_func=0, m_attn=0.25, m_mlp=1.0, rate=0.1, **kwargs):
+        self.d_model, self.attn_func = d_model, attn_func
+        self.fmha = FactorizedAttention(ctc_len, num_heads, d_model, blocks, attn_func=attn_func, m_attn=m_attn,
+                                        drop_out_rate=rate)
+        self.mlp_width = int(d_model * m_mlp)
+        if self.mlp_width != d_model:
+            raise ValueError("m_mlp != 1 changes the residual width (transformer.py:54-56 adds mlp output to x)")
+
+    def build(self, store: ParamStore, prefix: str):
+        d = self.d_model
+        self.prefix, self.store = prefix, store
+        store.add(f"{prefix}/ln1/gamma", (d,), "ones")
+        store.add(f"{prefix}/ln1/beta", (d,), "zeros")
+        self.fmha.build(store, prefix)
+        store.add(f"{prefix}/ln2/gamma", (d,), "ones")
+        store.add(f"{prefix}/ln2/beta", (d,), "zeros")
+        store.add(f"{prefix}/mlp/kernel", (d, self.mlp_width), "glorot_uniform")
+        store.add(f"{prefix}/mlp/bias", (self.mlp_width,), "zeros")
+
+    # -------------------------------------------------------------- forward / backward on the device
+    def forward(self, x, T, training, save, seed, salt, counter=None):
+        """x (N, T, d) -> (N, T, d). save: keep what backward needs (layer input, qkv, heads, lse, o32, x1)."""
+        f, cdt, eps = self.fmha, x.dtype, 1e-6
+        N = x.shape[0]
+        a = torch.empty_like(x)
+        V.layernorm_fwd(x, self.store.view(f"{self.prefix}/ln1/gamma"), self.store.view(f"{self.prefix}/ln1/beta"), a,
+                        eps)
+        w = f.width
+        qkv = torch.empty(N, T, 3 * w, dtype=cdt, device=x.device)
+        V.seqlin_fwd(a, f.p("qkv/kernel"), f.p("qkv/bias"), qkv, T, taps=3, dir=-1)
+        heads = []
+        for j, n in enumerate(("query", "key", "value")):
+            h = torch.empty(N, T, w, dtype=cdt, device=x.device)
+            V.seqlin_fwd(qkv[..., j * w:(j + 1) * w], f.p(f"mha/{n}/kernel"), f.p(f"mha/{n}/bias"), h, T)
+            heads.append(h)
+        qh, kh, vh = heads
+        oh = torch.empty_like(qh)
+        lse = torch.empty(N, T, f.num_heads, dtype=torch.float32, device=x.device)
+        V.attn_fwd(qh, kh, vh, oh, lse, f.attn_func, f.block_len, f.num_heads, 1.0 / math.sqrt(f.head_dim),
+                   vbias=f.p("mha/value/bias"))
+        o32 = torch.empty_like(qh)
+        V.seqlin_fwd(oh, f.p("mha/out/kernel"), f.p("mha/out/bias"), o32, T)
+        x1 = torch.empty_like(x)
+        drop = training and f.rate > 0
+        if drop:
+            V.seqlin_fwd(o32, f.p("proj/kernel"), f.p("proj/bias"), x1, T)
+            V.dropout_(x1, f.rate, seed, salt, counter)
+            V.axpy(x1, x, x1)
+        else:
+            V.seqlin_fwd(o32, f.p("proj/kernel"), f.p("proj/bias"), x1, T, residual=x)
+        h2 = torch.empty_like(x)
+        V.layernorm_fwd(x1, self.store.view(f"{self.prefix}/ln2/gamma"), self.store.view(f"{self.prefix}/ln2/beta"),
+                        h2, eps)
+        out = torch.empty_like(x)
+        V.seqlin_fwd(h2, self.store.view(f"{self.prefix}/mlp/kernel"), self.store.view(f"{self.prefix}/mlp/bias"),
+                     out, T, residual=x1)
+        self._saved = (x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter) if save else None
+        return out
+
+    def backward(self, dout, T, deferred, post_adds):
+        """dout = dL/d(out) -> dL/dx; weight gradients into the store (deferred partial reductions)."""
+        x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter = self._saved
+        self._saved = None
+        f, st, pre, eps = self.fmha, self.store, self.prefix, 1e-6
+        N, w, cdt = x.shape[0], f.width, x.dtype
+        # mlp: out = mlp(LN2(x1)) + x1
+        h2 = torch.empty_like(x)
+        V.layernorm_fwd(x1, st.view(f"{pre}/ln2/gamma"), st.view(f"{pre}/ln2/beta"), h2, eps)
+        dh2 = torch.empty_like(x)
+        V.seqlin_fwd(dout, st.view(f"{pre}/mlp/kernel"), None, dh2, T, wtrans=True)
+        V.seqlin_wgrad(h2, dout, st.grad_view(f"{pre}/mlp/kernel"), st.grad_view(f"{pre}/mlp/bias"), T,
+                       deferred=deferred)
+        dx1 = torch.empty_like(x)
+        V.layernorm_bwd(x1, dh2, st.view(f"{pre}/ln2/gamma"), dx1, st.grad_view(f"{pre}/ln2/gamma"),
+                        st.grad_view(f"{pre}/ln2/beta"), eps, deferred)
+        V.axpy(dx1, dout, dx1)
+        # x1 = x + dropout(proj(o32))
+        dres1 = dx1
+        if drop:
+            dres1 = dx1.clone()
+            V.dropout_(dres1, f.rate, seed, salt, counter)
+        do32 = torch.empty_like(qh)
+        V.seqlin_fwd(dres1, f.p("proj/kernel"), None, do32, T, wtrans=True)
+        V.seqlin_wgrad(o32, dres1, f.g("proj/kernel"), f.g("proj/bias"), T, deferred=deferred)
+        doh = torch.empty_like(qh)
+        V.seqlin_fwd(do32, f.p("mha/out/kernel"), None, doh, T, wtrans=True)
+        V.seqlin_wgrad(oh, do32, f.g("mha/out/kernel"), f.g("mha/out/bias"), T, deferred=deferred)
+        dqh, dkh, dvh = torch.empty_like(qh), torch.empty_like(qh), torch.empty_like(qh)
+        dsum = torch.empty(N, T, f.num_heads, dtype=torch.float32, device=x.device)
+        V.attn_bwd(qh, kh, vh, oh, lse, doh, dsum, dqh, dkh, dvh, f.attn_func, f.block_len, f.num_heads,
+                   1.0 / math.sqrt(f.head_dim))
+        if f.attn_func == 2:
+            # the zero block of block 0: its values are the value bias, d(bias) += sum of dO over block 0
+            tmp = torch.empty(f.block_len, w, dtype=torch.float32, device=x.device)
+            V.colsum(doh, tmp, N, T * w, f.block_len * w)
+            extra = torch.empty(w, dtype=torch.float32, device=x.device)
+            V.colsum(tmp, extra, f.block_len, w, w)
+            post_adds.append((f.g("mha/value/bias").view(-1), extra))
+        dqkv = torch.empty_like(qkv)
+        for j, (n, dh) in enumerate((("query", dqh), ("key", dkh), ("value", dvh))):
+            V.seqlin_fwd(dh, f.p(f"mha/{n}/kernel"), None, dqkv[..., j * w:(j + 1) * w], T, wtrans=True)
+            V.seqlin_wgrad(qkv[..., j * w:(j + 1) * w], dh, f.g(f"mha/{n}/kernel"), f.g(f"mha/{n}/bias"), T,
+                           deferred=deferred)
+        a = torch.empty_like(x)
+        V.layernorm_fwd(x, st.view(f"{pre}/ln1/gamma"), st.view(f"{pre}/ln1/beta"), a, eps)
+        da = torch.empty_like(x)
+        V.seqlin_fwd(dqkv, f.p("qkv/kernel"), None, da, T, taps=3, dir=1, wtrans=True)
+        V.seqlin_wgrad(a, dqkv, f.g("qkv/kernel"), f.g("qkv/bias"), T, taps=3, deferred=deferred)
+        dx = torch.empty_like(x)
+        V.layernorm_bwd(x, da, st.view(f"{pre}/ln1/gamma"), dx, st.grad_view(f"{pre}/ln1/gamma"),
+                        st.grad_view(f"{pre}/ln1/beta"), eps, deferred)
+        V.axpy(dx, dx1, dx)
+        return dx
+
+    def layer_desc(self):
+        st, pre = self.store, self.prefix
+        v = lambda n: st.view(f"{pre}/{n}").data_ptr()
+        return V.PriorLayerDesc(v("ln1/gamma"), v("ln1/beta"), v("qkv/kernel"), v("qkv/bias"), v("mha/query/kernel"),
+                                v("mha/query/bias"), v("mha/key/kernel"), v("mha/key/bias"), v("mha/value/kernel"),
+                                v("mha/value/bias"), v("mha/out/kernel"), v("mha/out/bias"), v("proj/kernel"),
+                                v("proj/bias"), v("ln2/gamma"), v("ln2/beta"), v("mlp/kernel"), v("mlp/bias"),
+                                self.attn_func)
+
+
+class FactorizedTransformer:
+    def __init__(self, ctc_len, num_heads, depth, d_model, blocks, attn_stacks, m_attn=0.25, m_mlp=1.0, rate=0.1,
+                 **kwargs):
+        self.d_model, self.depth = d_model, depth
+        self.attn_func = {0: lambda d: [0, 1][d % 2], 1: lambda d: [0, 1, 2][d % 3]}[attn_stacks]
+        self.layers = [ResidualAttnBlock(ctc_len, num_heads, d_model, blocks, attn_func=self.attn_func(i),
+                                         m_attn=m_attn, m_mlp=m_mlp, rate=rate) for i in range(depth)]
+
+    def build(self, store, prefix):
+        for i, ly in enumerate(self.layers):
+            ly.build(store, f"{prefix}/layer{i}")
+
+
+class LabelConditioner:
+    """label_conditioners.py:9-48: genre Embedding(genre_bins, width) -> (N, 1, width)."""
+
+    def __init__(self, genre_bins, width, **kwargs):
+        self.genre_bins, self.model = genre_bins, width
+
+    def build(self, store, prefix):
+        self.store, self.name = store, store.add(f"{prefix}/genre_embedding/embeddings", (self.genre_bins, self.model),
+                                                 "uniform")
+
+    def __call__(self, y, training=False, **kwargs):
+        y = torch.as_tensor(y, device=self.store.flat.device).long().reshape(-1)
+        return self.store.view(self.name)[y].unsqueeze(1)
+
+
+class FMHABasedAutoregressiveModel:
+    """autoregressive_fmha.py:13-240 on libvqa. dtype 'fp32' (parity) or 'bf16' (activations; fp32 weights)."""
+
+    def __init__(self, target_vocab_size, width, depth, blocks, m_attn=0.25, m_mlp=1.0, heads=1, attn_stacks=1,
+                 maximum_pos_encoding=5000, drop_out_rate=0.1, context_length=None, zq_shapes=None, level=0, levels=3,
+                 pos_emb=True, downs=None, strides=None, cond_kwargs=None, dtype="fp32", device="cuda", seed=1,
+                 store: Optional[ParamStore] = None, prefix="prior", **kwargs):
+        self.context_length = int(np.prod(context_length))
+        self.bins, self.d_model, self.depth = target_vocab_size, width, depth
+        self.heads, self.blocks = heads, blocks
+        self.use_pos_embedding = pos_emb
+        self.levels, self.level, self.cond_level = levels, level, level + 1
+        self.rate = drop_out_rate
+        self.start_token = self.bins - 1
+        self.cdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.device = torch.device(device)
+        self.cond_downsample_rate = (strides[self.cond_level] ** downs[self.cond_level]
+                                     if (strides is not None and self.level != levels - 1) else None)
+        self.transformer = FactorizedTransformer(self.context_length, heads, depth, width, blocks, attn_stacks,
+                                                 m_attn=m_attn, m_mlp=m_mlp, rate=drop_out_rate)
+        self.conditioner = None
+        if self.cond_level != levels and cond_kwargs is not None:
+            self.conditioner = ConditionerNet(cond_shape=zq_shapes[self.cond_level], bins=self.bins,
+                                              embed_width=self.d_model, down_depth=downs[self.cond_level],
+                                              stride=strides[self.cond_level], **cond_kwargs)
+        own = store is None
+        self.store = store if store is not None else ParamStore()
+        self.prefix = prefix
+        st = self.store
+        self.emb_name = st.add(f"{prefix}/x_embedding/embeddings", (self.bins, width), "uniform")
+        self.pos_name = (st.add(f"{prefix}/pos_embedding/embeddings", (self.context_length, width), "uniform")
+                         if pos_emb else None)
+        self.transformer.build(st, prefix)
+        self.out_kernel = st.add(f"{prefix}/out/kernel", (width, self.bins), "glorot_uniform")
+        self.out_bias = st.add(f"{prefix}/out/bias", (self.bins,), "zeros")
+        if self.conditioner is not None:
+            self.conditioner.build(st, f"{prefix}/conditioner", width, self.cdt)
+        if own:
+            st.materialize(self.device, seed=seed)
+        self._pos_table = None
+        if not pos_emb:
+            self._pos_table = torch.from_numpy(positional_encoding(maximum_pos_encoding, width)[0]).to(self.device)
+        self._counter = 0
+
+    # -------------------------------------------------------------- pieces
+    def _pos(self):
+        return self.store.view(self.pos_name) if self.use_pos_embedding else self._pos_table
+
+    def _wt(self, dtype):
+        wt = torch.empty(self.bins, self.d_model, dtype=dtype, device=self.device)
+        V.head_wt(self.store.view(self.out_kernel), wt)
+        return wt
+
+    def _embed(self, tokens, training, x_cond=None, y_cond=None, seed=0, counter=None):
+        N, T = tokens.shape
+        x = torch.empty(N, T, self.d_model, dtype=self.cdt, device=self.device)
+        V.prior_embed_fwd(self.store.view(self.emb_name), self._pos(), tokens, x, math.sqrt(self.d_model),
+                          ycond=y_cond, xcond=x_cond, rate=self.rate if training else 0.0, seed=seed, counter=counter)
+        return x
+
+    def hidden(self, tokens, training=False, x_cond=None, y_cond=None, save=False, seed=0, counter=None):
+        """Embedding + transformer: (N, T) tokens -> (N, T, d) final hidden state (the head's input)."""
+        tokens = tokens.contiguous()
+        T = tokens.shape[1]
+        if self.use_pos_embedding and T > self.context_length:
+            raise ValueError(f"sequence of {T} > context length {self.context_length}")
+        x = self._embed(tokens, training, x_cond, y_cond, seed, counter)
+        for i, ly in enumerate(self.transformer.layers):
+            x = ly.forward(x, T, training, save, seed, 1000 + i, counter)
+        return x
+
+    def _cond(self, x_cond, save=False):
+        if x_cond is None:
+            return None
+        x_cond = torch.as_tensor(x_cond, device=self.device)
+        if x_cond.dim() == 3:  # already up-sampled (autoregressive_fmha.py:145-148)
+            return x_cond.to(self.cdt).contiguous()
+        return self.conditioner.forward(x_cond.long().contiguous(), save=save)
+
+    # -------------------------------------------------------------- Keras-like call / sample
+    def __call__(self, x, training=False, x_cond=None, y_cond=None):
+        """autoregressive_fmha.py:109-160 -> ((N, T, bins) fp32 logits, {}). Logits are materialised here (the
+        training step never does): 128-wide vocab slices of the head as sequence-linear launches."""
+        tokens = torch.as_tensor(x, device=self.device).long()
+        with torch.no_grad():
+            h = self.hidden(tokens, training, self._cond(x_cond), self._ycond(y_cond))
+            N, T = tokens.shape
+            wt32 = torch.empty(self.bins, self.d_model, dtype=torch.float32, device=self.device)
+            V.head_wt(self.store.view(self.out_kernel), wt32)
+            hf = h.float().contiguous()
+            logits = torch.empty(N, T, self.bins, dtype=torch.float32, device=self.device)
+            b = self.store.view(self.out_bias)
+            for v0 in range(0, self.bins, 128):
+                n = min(128, self.bins - v0)
+                if n % 16:
+                    raise ValueError("bins must be a multiple of 16 to materialise logits")
+                V.seqlin_fwd(hf, wt32[v0:v0 + n], b[v0:v0 + n], logits[..., v0:v0 + n], T, wtrans=True)
+        return logits, {}
+
+    call = __call__
+
+    def _ycond(self, y_cond):
+        if y_cond is None:
+            return None
+        return torch.as_tensor(y_cond, device=self.device, dtype=torch.float32).reshape(-1, self.d_model).contiguous()
+
+    def decode_cache(self, n_samples):
+        nbytes = V.lib().vqa_prior_decode_cache_bytes(n_samples, self.depth, self.context_length)
+        return torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+
+    def sample(self, n_samples, max_length=None, x_cond=None, y_cond=None, return_attention_weights=False, seed=0,
+               forced=None, return_logits=False):
+        """autoregressive_fmha.py:162-240: (N, max_length + 1) int64 tokens starting with the start token, each
+        next token = argmax(logits + Gumbel noise). One persistent decode launch."""
+        L = self.context_length if max_length is None else int(max_length)
+        xc = None
+        if x_cond is not None:
+            xc = self._cond(x_cond).float().contiguous()
+            if xc.shape[:2] != (n_samples, self.context_length) and xc.shape[1] < L:
+                raise ValueError(f"x_cond shape {tuple(xc.shape)} does not cover {L} positions")
+            if xc.shape[1] != self.context_length:
+                full = torch.zeros(n_samples, self.context_length, self.d_model, device=self.device)
+                full[:, :xc.shape[1]] = xc
+                xc = full
+        tokens = torch.empty(n_samples, L + 1, dtype=torch.int64, device=self.device)
+        logits = (torch.empty(n_samples, L, self.bins, dtype=torch.float32, device=self.device)
+                  if return_logits else None)
+        if forced is not None:
+            forced = torch.as_tensor(forced, device=self.device).long().contiguous()
+        layers = [ly.layer_desc() for ly in self.transformer.layers]
+        V.prior_decode(layers, self.store.view(self.emb_name), self._pos().contiguous(),
+                       self.store.view(self.out_kernel), self.store.view(self.out_bias), tokens,
+                       self.decode_cache(n_samples), L, self.context_length, self.heads, self.blocks,
+                       self.start_token, seed, ycond=self._ycond(y_cond), xcond=xc, forced=forced, logits=logits)
+        if return_logits:
+            return tokens, logits
+        return tokens
+
+    @property
+    def trainable_variables(self):
+        return [self.store.view(n) for n, _, _ in self.store.specs if n.startswith(self.prefix + "/")]
+
+
+class Prior:
+    """prior.py:102-372: trains one level's FMHABasedAutoregressiveModel on the VQ-VAE's codes.
+
+    train_step(x) takes raw audio (N, T, 1) (encoded with `vqvae_model`) or the codes themselves (N, T_l) int64.
+    Returns {"loss", "perplexity(per word)", "accuracy"} running means (device tensors)."""
+
+    def __init__(self, level, z_shapes, bins, down_depth, strides, vqvae_model, prior_kwargs, x_cond_kwargs,
+                 prior_monitor=None, genre_classes=None, dtype="fp32", device="cuda", seed=1, learning_rate=1e-3,
+                 **kwargs):
+        assert len(down_depth) == len(strides) == len(z_shapes)
+        self.level, self.z_shapes, self.levels = level, z_shapes, len(z_shapes)
+        self.z_shape = z_shapes[level]
+        self.context_length = int(np.prod(self.z_shape))
+        self.bins, self.genre_bins = bins, genre_classes
+        self.vqvae = vqvae_model
+        self.device = torch.device(device)
+        self.prior = FMHABasedAutoregressiveModel(
+            target_vocab_size=bins, width=prior_kwargs["width"], depth=prior_kwargs["depth"],
+            heads=prior_kwargs["heads"], blocks=prior_kwargs["blocks"], attn_stacks=prior_kwargs["attn_stacks"],
+            drop_out_rate=prior_kwargs.get("drop_out_rate", 0.1), context_length=self.z_shape, zq_shapes=z_shapes,
+            level=level, levels=self.levels, downs=down_depth, strides=strides, cond_kwargs=x_cond_kwargs,
+            dtype=dtype, device=device, seed=seed)
+        self.label_conditioner = None
+        if genre_classes is not None:
+            raise NotImplementedError("label-conditioned training (LabelConditioner) is not built yet; the sampler "
+                                      "takes y_cond")
+        self.optimizer = Adam(learning_rate=learning_rate)
+        self.optimizer.build(self.prior.store)  # its device step counter also drives dropout / teacher forcing
+        self.train_loss_tracker = Mean("train_loss", self.device)
+        self.train_accuracy_tracker = Mean("train_accuracy", self.device)
+        self.train_monitor = prior_monitor
+        self.teacher_seed = 3
+        self._step = 0
+        self._graph = None
+        self._scalars = torch.zeros(2, dtype=torch.float32, device=self.device)
+
+    @property
+    def metrics(self):
+        return [self.train_loss_tracker, self.train_accuracy_tracker]
+
+    def reset_metrics(self):
+        for m in self.metrics:
+            m.reset_state()
+
+    def set_train_monitor(self, train_monitor):
+        self.train_monitor = train_monitor
+
+    def get_cond(self, zs, start, end):
+        """autoregressive_fmha.py:82-105."""
+        if self.level == self.levels - 1:
+            return None
+        r = self.prior.cond_downsample_rate
+        assert start % r == end % r == 0
+        return zs[self.level + 1][:, start // r:end // r]
+
+    def _codes(self, x):
+        if isinstance(x, tuple):
+            x = x[0]
+        x = torch.as_tensor(x, device=self.device)
+        if x.dtype == torch.int64:
+            return x.contiguous(), None
+        codes = self.vqvae.encode(x, start_level=self.level, end_level=self.levels)
+        upper = codes[1] if self.level != self.levels - 1 else None
+        return codes[0].contiguous(), upper
+
+    def results(self):
+        loss = self.train_loss_tracker.result()
+        return {"loss": loss, "perplexity(per word)": torch.exp(loss), "accuracy": self.train_accuracy_tracker.result()}
+
+    # -------------------------------------------------------------- the step
+    def _compute(self, codes, upper, teacher_force_rate, tf_mask=None, apply=True):
+        m, st = self.prior, self.prior.store
+        N, T = codes.shape
+        M = N * T
+        dev = self.device
+        seed = self.teacher_seed
+        ctr = self.optimizer.iterations
+        xc = m._cond(upper, save=True) if upper is not None else None
+        # pass 1: teacher-forced input, argmax of the logits (prior.py:277-282)
+        latent = torch.empty_like(codes)
+        V.tf_mix(codes, None, None, latent, m.start_token)
+        wt = m._wt(m.cdt)
+        b = st.view(m.out_bias)
+        with torch.no_grad():
+            h0 = m.hidden(latent, True, xc, seed=seed * 7919 + 1, counter=ctr)
+            lse0 = torch.empty(M, dtype=torch.float32, device=dev)
+            amax = torch.empty(N, T, dtype=torch.int64, device=dev)
+            V.head_fwd(h0, wt, b, lse0, amax=amax)
+            del h0
+        # mix (prior.py:283-290) and pass 2 with gradients
+        batch_input = torch.empty_like(codes)
+        mask = None if tf_mask is None else torch.as_tensor(tf_mask, device=dev).to(torch.uint8).contiguous()
+        V.tf_mix(codes, amax, mask, batch_input, m.start_token, rate=float(teacher_force_rate), seed=seed,
+                 counter=ctr)
+        h = m.hidden(batch_input, True, xc, save=True, seed=seed * 7919 + 2, counter=ctr)
+        lse = torch.empty(M, dtype=torch.float32, device=dev)
+        loss_row = torch.empty(M, dtype=torch.float32, device=dev)
+        correct = torch.empty(M, dtype=torch.float32, device=dev)
+        V.head_fwd(h, wt, b, lse, targets=codes, loss_row=loss_row, correct=correct)
+        V.rowsum(loss_row, 1, M, 1.0 / M, self._scalars[0:1])
+        V.rowsum(correct, 1, M, 1.0 / M, self._scalars[1:2])
+        self._last_batch_input = batch_input
+        if not apply:
+            return
+        deferred = V.Deferred()
+        st.deferred = deferred
+        post = []
+        try:
+            dh = torch.empty_like(h)
+            V.head_bwd(h, wt, b, codes, lse, 1.0 / M, dh, st.grad_view(m.out_kernel), st.grad_view(m.out_bias),
+                       deferred=deferred)
+            for ly in reversed(m.transformer.layers):
+                dh = ly.backward(dh, T, deferred, post)
+            # embeddings: x0 = E[tok] * sqrt(d) + pos (+ x_cond)
+            gt = st.grad_view(m.emb_name)
+            gt.zero_()
+            V.embedding_bwd(dh, batch_input, gt)
+            if m.use_pos_embedding:
+                V.colsum(dh, st.grad_view(m.pos_name), N, T * m.d_model, T * m.d_model)
+            if xc is not None:
+                m.conditioner.backward(dh)
+            deferred.flush()
+            V.scale_f32_(gt, math.sqrt(m.d_model))
+            for dst, extra in post:
+                V.axpy(dst, extra, dst)
+        finally:
+            st.deferred = None
+        if m.use_pos_embedding and T < m.context_length:
+            st.grad_view(m.pos_name)[T:].zero_()
+        self.optimizer.apply(st)
+
+    def _update_metrics(self):
+        self.train_loss_tracker.update_state(self._scalars[0])
+        self.train_accuracy_tracker.update_state(self._scalars[1])
+
+    def train_step(self, x, teacher_force_rate=0.2, tf_mask=None):
+        """prior.py:241-335. tf_mask (N, T) bool overrides the random teacher-forcing draw (parity tests)."""
+        codes, upper = self._codes(x)
+        if self._graph is not None and tf_mask is None and codes.shape == self._graph_codes.shape:
+            self._graph_codes.copy_(codes)
+            self._graph.replay()
+            self._step += 1
+            return self.results()
+        self._compute(codes, upper, teacher_force_rate, tf_mask)
+        self._update_metrics()
+        self._step += 1
+        return self.results()
+
+    def test_step(self, x):
+        """prior.py:337-372: loss / accuracy of the teacher-forced input (no mixing, no update)."""
+        m = self.prior
+        codes, upper = self._codes(x)
+        N, T = codes.shape
+        M = N * T
+        with torch.no_grad():
+            latent = torch.empty_like(codes)
+            V.tf_mix(codes, None, None, latent, m.start_token)
+            h = m.hidden(latent, False, m._cond(upper))
+            lse = torch.empty(M, dtype=torch.float32, device=self.device)
+            lr, cr = torch.empty_like(lse), torch.empty_like(lse)
+            V.head_fwd(h, m._wt(m.cdt), m.store.view(m.out_bias), lse, targets=codes, loss_row=lr, correct=cr)
+            out = torch.empty(2, dtype=torch.float32, device=self.device)
+            V.rowsum(lr, 1, M, 1.0 / M, out[0:1])
+            V.rowsum(cr, 1, M, 1.0 / M, out[1:2])
+        return {"loss": out[0], "perplexity(per word)": torch.exp(out[0]), "accuracy": out[1]}
+
+    def capture_train_step(self, codes_example, teacher_force_rate=0.2, warmup=1):
+        """Record the whole step (both passes, backward, Adam, metrics) as one hipGraph; later train_step calls
+        with this shape copy the codes in and replay (the teacher-forcing draw advances on the device)."""
+        codes, upper = self._codes(codes_example)
+        if upper is not None:
+            raise NotImplementedError("graph capture of the conditioned prior step")
+        self._graph_codes = codes.clone()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._compute(self._graph_codes, None, teacher_force_rate)
+                self._update_metrics()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._compute(self._graph_codes, None, teacher_force_rate)
+            self._update_metrics()
+        self._graph = g
+        torch.cuda.synchronize(self.device)
+
+    def sample(self, n_samples, z_cond=None, y=None, return_attn_weights=False, seed=0):
+        """prior.py:374-400: one window of n_ctx tokens (without the start token)."""
+        out = self.prior.sample(n_samples, x_cond=z_cond, y_cond=y, seed=seed)
+        return out[:, 1:]

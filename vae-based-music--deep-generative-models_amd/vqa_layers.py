@@ -46,8 +46,11 @@ class ParamStore:
         vals = {}
         for name, shape, init in self.specs:
             if init == "glorot_uniform":
-                K = shape[0]
-                lim = math.sqrt(6.0 / (K * shape[1] + K * shape[2]))
+                if len(shape) == 2:  # Dense kernel (in, out)
+                    lim = math.sqrt(6.0 / (shape[0] + shape[1]))
+                else:  # keras fans of an N-D kernel: receptive field prod(shape[:-2])
+                    rf = int(np.prod(shape[:-2]))
+                    lim = math.sqrt(6.0 / (rf * shape[-2] + rf * shape[-1]))
                 vals[name] = rng.uniform(-lim, lim, size=shape).astype(np.float32)
             elif init == "uniform":
                 vals[name] = rng.uniform(-0.05, 0.05, size=shape).astype(np.float32)

@@ -36,6 +36,10 @@ EXPORTED = [
     "vqa_step_metrics", "vqa_synthetic_batch",
     "vqa_embedding_fwd", "vqa_embedding_bwd", "vqa_embedding_bwd_workspace", "vqa_layernorm_fwd",
     "vqa_layernorm_bwd", "vqa_layernorm_bwd_workspace",
+    "vqa_seqlin_fwd", "vqa_seqlin_wgrad_workspace", "vqa_seqlin_wgrad", "vqa_prior_embed_fwd", "vqa_colsum",
+    "vqa_axpy", "vqa_dropout", "vqa_scale_f32", "vqa_tf_mix", "vqa_attn_fwd", "vqa_attn_bwd", "vqa_head_wt",
+    "vqa_head_fwd", "vqa_head_bwd_workspace", "vqa_head_bwd", "vqa_rowsum", "vqa_prior_decode_cache_bytes",
+    "vqa_prior_decode",
 ]
 
 
@@ -109,6 +113,25 @@ _SIGS = {
     "vqa_spectral_target": (_I, [_P, _P, _S, _I, _I, _P, _P, _P, _I, _P]),
     "vqa_spectral_loss_target_workspace": (_S, [_I, _I, _P, _P, _P, _I, _I]),
     "vqa_spectral_loss_target": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _S, _P]),
+    # factorized-attention prior
+    "vqa_seqlin_fwd": (_I, [_P, _L, _P, _P, _P, _L, _P, _L] + [_I] * 9 + [_P]),
+    "vqa_seqlin_wgrad_workspace": (_S, [_I] * 5),
+    "vqa_seqlin_wgrad": (_I, [_P, _L, _P, _L, _P, _P] + [_I] * 6 + [_P, _S, _P, _P]),
+    "vqa_prior_embed_fwd": (_I, [_P] * 6 + [_I] * 4 + [_F, _F, _U, _P, _I, _P]),
+    "vqa_colsum": (_I, [_P, _P, _I, _L, _L, _I, _I, _P]),
+    "vqa_axpy": (_I, [_P, _P, _P, _L, _I, _P]),
+    "vqa_dropout": (_I, [_P, _L, _F, _U, _U, _P, _I, _P]),
+    "vqa_scale_f32": (_I, [_P, _L, _F, _P]),
+    "vqa_tf_mix": (_I, [_P, _P, _P, _P, _I, _I, _L, _F, _U, _U, _P, _P]),
+    "vqa_attn_fwd": (_I, [_P] * 6 + [_I] * 6 + [_F, _I, _P]),
+    "vqa_attn_bwd": (_I, [_P] * 10 + [_I] * 6 + [_F, _I, _P]),
+    "vqa_head_wt": (_I, [_P, _P, _I, _I, _I, _P]),
+    "vqa_head_fwd": (_I, [_P] * 8 + [_L, _I, _I, _I, _P]),
+    "vqa_head_bwd_workspace": (_S, [_L, _I, _I]),
+    "vqa_head_bwd": (_I, [_P] * 5 + [_F, _P, _P, _P, _L, _I, _I, _I, _P, _S, _P, _P]),
+    "vqa_rowsum": (_I, [_P, _L, _L, _F, _P, _P]),
+    "vqa_prior_decode_cache_bytes": (_S, [_I, _I, _I]),
+    "vqa_prior_decode": (_I, [_P, _I] + [_P] * 10 + [_S] + [_I] * 7 + [_L, _U, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -502,3 +525,136 @@ def spectral_loss_target(target, r, loss_out, dr, item_loss, n_fft, hop, win, ws
 def stft_magnitude(x, mag, n_fft, hop, win):
     B, T = x.shape[0], x.numel() // x.shape[0]
     _check(lib().vqa_stft_magnitude(ptr(x), ptr(mag), B, T, n_fft, hop, win, stream()), "vqa_stft_magnitude")
+
+
+# ---- factorized-attention prior (vqa_prior.hip) -----------------------------------------------------
+def rptr(t: torch.Tensor):
+    """(pointer, row stride) of a row-strided view (last dim contiguous, uniform row stride): column slices
+    such as qkv[..., 0:32] of a (N, T, 96) tensor."""
+    if not t.is_cuda:
+        raise VQAError("libvqa ops take device tensors only (got a CPU tensor)")
+    if t.stride(-1) != 1:
+        raise VQAError("row-strided view needs a contiguous last dimension")
+    ld = t.stride(-2) if t.dim() >= 2 else t.shape[-1]
+    for d in range(t.dim() - 2):
+        if t.stride(d) != t.stride(d + 1) * t.shape[d + 1]:
+            raise VQAError(f"view with strides {t.stride()} is not row-strided")
+    return ctypes.c_void_p(t.data_ptr()), ld
+
+
+def seqlin_fwd(x, w, b, y, T, taps=1, dir=-1, wtrans=False, residual=None, accumulate=False):
+    """vqa_seqlin_fwd on (nseq*T, K) rows -> (nseq*T, N) rows. w: (taps, K, N) (wtrans: (taps, N, K)) or (K, N)."""
+    px, ldx = rptr(x)
+    py, ldy = rptr(y)
+    pr, ldr = rptr(residual) if residual is not None else (None, 0)
+    K, N = x.shape[-1], y.shape[-1]
+    rows = x.numel() // K
+    _check(lib().vqa_seqlin_fwd(px, ldx, ptr(w), ptr(b), pr, ldr, py, ldy, rows // T, T, K, N, taps, dir,
+                                int(bool(wtrans)), int(bool(accumulate)), dtype_code(x.dtype), stream()),
+           "vqa_seqlin_fwd")
+
+
+def seqlin_wgrad(x, dy, dw, db, T, taps=1, deferred=None):
+    px, ldx = rptr(x)
+    pd, ldd = rptr(dy)
+    K, N = x.shape[-1], dy.shape[-1]
+    nseq = (x.numel() // K) // T
+    ws = workspace(lib().vqa_seqlin_wgrad_workspace(nseq, T, K, N, taps), x.device)
+    d = PartialsDesc() if deferred is not None else None
+    _check(lib().vqa_seqlin_wgrad(px, ldx, pd, ldd, ptr(dw), ptr(db), nseq, T, K, N, taps, dtype_code(x.dtype),
+                                  ptr(ws), ws.numel(), ctypes.byref(d) if d is not None else None, stream()),
+           "vqa_seqlin_wgrad")
+    if deferred is not None:
+        deferred.add(d, ws)
+
+
+def prior_embed_fwd(table, pos, tokens, out, scale, ycond=None, xcond=None, rate=0.0, seed=0, counter=None):
+    N, T = tokens.shape
+    bins, W = table.shape
+    _check(lib().vqa_prior_embed_fwd(ptr(table), ptr(pos), ptr(tokens), ptr(ycond), ptr(xcond), ptr(out), N, T, W,
+                                     bins, scale, rate, seed, ptr(counter), dtype_code(out.dtype), stream()),
+           "vqa_prior_embed_fwd")
+
+
+def colsum(x, out, nout, ostride, inner, accumulate=False):
+    _check(lib().vqa_colsum(ptr(x), ptr(out), nout, ostride, inner, int(bool(accumulate)), dtype_code(x.dtype),
+                            stream()), "vqa_colsum")
+
+
+def axpy(x, y, z):
+    _check(lib().vqa_axpy(ptr(x), ptr(y), ptr(z), x.numel(), dtype_code(x.dtype), stream()), "vqa_axpy")
+
+
+def dropout_(x, rate, seed, salt, counter=None):
+    _check(lib().vqa_dropout(ptr(x), x.numel(), rate, seed, salt, ptr(counter), dtype_code(x.dtype), stream()),
+           "vqa_dropout")
+
+
+def scale_f32_(x, s):
+    _check(lib().vqa_scale_f32(ptr(x), x.numel(), s, stream()), "vqa_scale_f32")
+
+
+def tf_mix(codes, amax, mask, out, start, rate=0.0, seed=0, step=0, counter=None):
+    N, T = codes.shape
+    _check(lib().vqa_tf_mix(ptr(codes), ptr(amax), ptr(mask), ptr(out), N, T, start, rate, seed, step, ptr(counter),
+                            stream()), "vqa_tf_mix")
+
+
+def attn_fwd(q, k, v, o, lse, mode, l, heads, scale, vbias=None):
+    N, T, C = q.shape
+    _check(lib().vqa_attn_fwd(ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(vbias), N, T, heads, C // heads, l, mode,
+                              scale, dtype_code(q.dtype), stream()), "vqa_attn_fwd")
+
+
+def attn_bwd(q, k, v, o, lse, dout, dsum, dq, dk, dv, mode, l, heads, scale):
+    N, T, C = q.shape
+    _check(lib().vqa_attn_bwd(ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), ptr(dout), ptr(dsum), ptr(dq), ptr(dk),
+                              ptr(dv), N, T, heads, C // heads, l, mode, scale, dtype_code(q.dtype), stream()),
+           "vqa_attn_bwd")
+
+
+def head_wt(w, wt):
+    K, V = w.shape
+    _check(lib().vqa_head_wt(ptr(w), ptr(wt), K, V, dtype_code(wt.dtype), stream()), "vqa_head_wt")
+
+
+def head_fwd(x, wt, bias, lse, amax=None, targets=None, loss_row=None, correct=None):
+    K = x.shape[-1]
+    M = x.numel() // K
+    _check(lib().vqa_head_fwd(ptr(x), ptr(wt), ptr(bias), ptr(targets), ptr(lse), ptr(amax), ptr(loss_row),
+                              ptr(correct), M, K, wt.shape[0], dtype_code(x.dtype), stream()), "vqa_head_fwd")
+
+
+def head_bwd(x, wt, bias, targets, lse, inv_count, dx, dw, db, deferred=None):
+    K = x.shape[-1]
+    M = x.numel() // K
+    V = wt.shape[0]
+    ws = workspace(lib().vqa_head_bwd_workspace(M, K, V), x.device)
+    d = PartialsDesc() if deferred is not None else None
+    _check(lib().vqa_head_bwd(ptr(x), ptr(wt), ptr(bias), ptr(targets), ptr(lse), inv_count, ptr(dx), ptr(dw),
+                              ptr(db), M, K, V, dtype_code(x.dtype), ptr(ws), ws.numel(),
+                              ctypes.byref(d) if d is not None else None, stream()), "vqa_head_bwd")
+    if deferred is not None:
+        deferred.add(d, ws)
+
+
+def rowsum(x, rows, n, scale, out):
+    _check(lib().vqa_rowsum(ptr(x), rows, n, scale, ptr(out), stream()), "vqa_rowsum")
+
+
+class PriorLayerDesc(ctypes.Structure):
+    """vqa_prior_layer (include/vqa.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "ln1_gamma", "ln1_beta", "qkv_kernel", "qkv_bias", "query_kernel", "query_bias", "key_kernel", "key_bias",
+        "value_kernel", "value_bias", "out_kernel", "out_bias", "proj_kernel", "proj_bias", "ln2_gamma", "ln2_beta",
+        "mlp_kernel", "mlp_bias")] + [("attn_type", ctypes.c_int)]
+
+
+def prior_decode(layers, emb, pos, out_w, out_b, tokens, cache, steps, ctx, heads, blocks, start, seed, ycond=None,
+                 xcond=None, forced=None, logits=None):
+    N = tokens.shape[0]
+    arr = (PriorLayerDesc * len(layers))(*layers)
+    _check(lib().vqa_prior_decode(arr, len(layers), ptr(emb), ptr(pos), ptr(out_w), ptr(out_b), ptr(ycond),
+                                  ptr(xcond), ptr(forced), ptr(logits), ptr(tokens), ptr(cache), cache.numel(), N,
+                                  steps, ctx, emb.shape[1], heads, blocks, out_w.shape[1], start, seed, stream()),
+           "vqa_prior_decode")
