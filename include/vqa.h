@@ -337,8 +337,10 @@ size_t vqa_head_bwd_workspace(int64_t M, int K, int V);
 int vqa_head_bwd(const void* x, const void* wt, const float* bias, const int64_t* targets, const float* lse,
                  float inv_count, void* dx, float* dw, float* db, int64_t M, int K, int V, int dtype, void* workspace,
                  size_t ws_bytes, vqa_partials_desc* desc, vqa_stream_t stream);
-/* out[i] = scale * sum_j x[i*n + j] (fixed order). */
-int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, float* out, vqa_stream_t stream);
+/* out[i] = scale * sum_j x[i*n + j] (fixed-order two-stage reduction; workspace vqa_rowsum_workspace bytes). */
+size_t vqa_rowsum_workspace(int64_t rows, int64_t n);
+int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, float* out, void* workspace, size_t ws_bytes,
+               vqa_stream_t stream);
 
 /* Autoregressive sampling (autoregressive_fmha.py:162-240, Sampler.py): one persistent workgroup per sample
  * walks `steps` positions with a key/value cache, z = logits + Gumbel(uniform(seed, sample, step, bin)),

@@ -1003,12 +1003,23 @@ __global__ __launch_bounds__(256) void head_wt_kernel(const float* w, T* wt, int
   }
 }
 
-// out[i] = scale * sum_j x[i * n + j] (one workgroup per output, fixed order: deterministic)
-__global__ __launch_bounds__(256) void rowsum_kernel(const float* x, long long n, float scale, float* out) {
+// out[i] = scale * sum_j x[i * n + j]: stage 1 sums fixed chunks of 4096 per workgroup, stage 2 sums the chunk
+// results in order (deterministic)
+constexpr int kRowsumChunk = 4096;
+__global__ __launch_bounds__(256) void rowsum_part_kernel(const float* x, long long n, int nch, float* part) {
   __shared__ float red[4];
-  const float* p = x + (long long)blockIdx.x * n;
+  const int row = blockIdx.x / nch, ch = blockIdx.x - row * nch;
+  const float* p = x + (long long)row * n;
+  const long long j0 = (long long)ch * kRowsumChunk, j1 = std::min<long long>(n, j0 + kRowsumChunk);
   float s = 0.f;
-  for (long long j = threadIdx.x; j < n; j += 256) s += p[j];
+  for (long long j = j0 + threadIdx.x; j < j1; j += 256) s += p[j];
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void rowsum_final_kernel(const float* part, int nch, float scale, float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int j = threadIdx.x; j < nch; j += 256) s += part[(long long)blockIdx.x * nch + j];
   s = block_sum_256(s, red);
   if (threadIdx.x == 0) out[blockIdx.x] = s * scale;
 }
@@ -1047,30 +1058,35 @@ struct DecArgs {
   float scale, emb_scale, eps;
 };
 
-// y[o] = b[o] + sum_k x[k] W[k][o] (W row-major (K, O)); O <= 256 splits K over 256/O thread groups combined
-// in a fixed order; larger O: each thread owns outputs o = tid + 256 j
+// y[o] = b[o] + sum_k x[k] W[k][o] (W row-major (K, O), O % 4 == 0): thread (4-output chunk c, k-group kg) sums
+// its rows with 16-byte weight loads (many loads in flight per thread), then the k-groups are combined in a
+// fixed order. scr holds >= 256 * 4 floats.
 __device__ void dec_matvec(const float* x, int K, const float* W, const float* b, float* y, int O, float* scr) {
-  const int tid = threadIdx.x;
-  if (O <= 256) {
-    const int G = 256 / O, grp = tid / O, o = tid - grp * O;
-    if (grp < G) {
-      const int k0 = grp * K / G, k1 = (grp + 1) * K / G;
-      float s = 0.f;
-      for (int k = k0; k < k1; ++k) s += x[k] * W[(size_t)k * O + o];
-      scr[grp * O + o] = s;
+  const int tid = threadIdx.x, nc = O / 4;
+  if (nc <= 256) {
+    const int G = 256 / nc, kg = tid / nc, c = tid - kg * nc;
+    if (kg < G) {
+      const int k0 = kg * K / G, k1 = (kg + 1) * K / G;
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int k = k0; k < k1; ++k) s = s + x[k] * *(const f32x4*)(W + (size_t)k * O + 4 * c);
+      *(f32x4*)(scr + (kg * nc + c) * 4) = s;
     }
     __syncthreads();
-    if (tid < O) {
-      float s = scr[tid];
-      for (int gg = 1; gg < G; ++gg) s += scr[gg * O + tid];
-      y[tid] = s + (b ? b[tid] : 0.f);
+    if (tid < nc) {
+      f32x4 s = *(const f32x4*)(scr + tid * 4);
+      for (int g = 1; g < G; ++g) s = s + *(const f32x4*)(scr + (g * nc + tid) * 4);
+      if (b) s = s + *(const f32x4*)(b + 4 * tid);
+      *(f32x4*)(y + 4 * tid) = s;
     }
     __syncthreads();
   } else {
-    for (int o = tid; o < O; o += 256) {
-      float s = 0.f;
-      for (int k = 0; k < K; ++k) s += x[k] * W[(size_t)k * O + o];
-      y[o] = s + (b ? b[o] : 0.f);
+    for (int c = tid; c < nc; c += 256) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 16
+      for (int k = 0; k < K; ++k) s = s + x[k] * *(const f32x4*)(W + (size_t)k * O + 4 * c);
+      if (b) s = s + *(const f32x4*)(b + 4 * c);
+      *(f32x4*)(y + 4 * c) = s;
     }
     __syncthreads();
   }
@@ -1092,13 +1108,15 @@ __device__ void dec_layernorm(const float* x, const float* gm, const float* bt, 
 }
 
 __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
-  __shared__ float x[kDecW], x1[kDecW], hb[kDecW], r1[kDecW];
+  __shared__ __attribute__((aligned(16))) float x[kDecW], x1[kDecW], hb[kDecW], r1[kDecW];
   __shared__ float ring[kDecMaxLayers][3][kDecW];
-  __shared__ float cat[3 * kDecW], qkv[3 * kDecAW], qh[kDecAW], kh[kDecAW], vh[kDecAW], oh[kDecAW], o32[kDecAW];
+  __shared__ __attribute__((aligned(16))) float cat[3 * kDecW], qkv[3 * kDecAW], qh[kDecAW], kh[kDecAW], vh[kDecAW],
+      oh[kDecAW], o32[kDecAW];
   __shared__ float sc[2][kDecMaxL];
-  __shared__ float scr[2048];
-  __shared__ float stat[4], red[8][kDecAW];
-  __shared__ float bestv[256];
+  __shared__ __attribute__((aligned(16))) float scr[2048];
+  __shared__ __attribute__((aligned(16))) float red[32][kDecAW];
+  __shared__ float stat[4];
+  __shared__ __attribute__((aligned(16))) float bestv[1024];
   __shared__ int besti[256];
   const int n = blockIdx.x, tid = threadIdx.x;
   for (int e = tid; e < kDecMaxLayers * 3 * kDecW; e += 256) (&ring[0][0][0])[e] = 0.f;
@@ -1177,17 +1195,20 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
           if (lane == 0) stat[wave] = 1.0f / su;
         }
         __syncthreads();
-        // o[h][d] = sum_j p_j v_j[h][d]: thread (c = tid & 31, slice = tid >> 5) over keys slice, slice+8, ...
+        // o[h][d] = sum_j p_j v_j[h][d]: thread (4-channel chunk c4 = tid & 7, key slice sl = tid >> 3) over keys
+        // sl, sl + 32, ... with 16-byte loads; slices combined in a fixed order
         {
-          const int c = tid & 31, sl = tid >> 5, h = c / hd;
-          float acc = 0.f;
-          for (int idx = sl; idx < cnt; idx += 8) acc += sc[h][idx] * vcL[(size_t)(j0 + idx * jstep) * kDecAW + c];
-          red[sl][c] = acc;
+          const int c4 = tid & 7, sl = tid >> 3, h = 4 * c4 / hd;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+          for (int idx = sl; idx < cnt; idx += 32)
+            acc = acc + sc[h][idx] * *(const f32x4*)(vcL + (size_t)(j0 + idx * jstep) * kDecAW + 4 * c4);
+          *(f32x4*)(&red[sl][4 * c4]) = acc;
         }
         __syncthreads();
         if (tid < kDecAW) {
           float o = red[0][tid];
-          for (int sl = 1; sl < 8; ++sl) o += red[sl][tid];
+          for (int sl = 1; sl < 32; ++sl) o += red[sl][tid];
           oh[tid] = o * stat[tid / hd];
         }
         __syncthreads();
@@ -1202,7 +1223,7 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
       __syncthreads();
     }
     // output head + Gumbel-max
-    dec_matvec(x, kDecW, a.hw, a.hb, scr, a.bins, bestv);  // bins > 256: scr holds the logits
+    dec_matvec(x, kDecW, a.hw, a.hb, scr, a.bins, bestv);  // scr holds the logits
     float bv = -INFINITY;
     int bi = 0;
     for (int v = tid; v < a.bins; v += 256) {
@@ -1547,9 +1568,20 @@ extern "C" int vqa_head_bwd(const void* x, const void* wt, const float* bias, co
   return vqa_reduce_partials(&d, 1, stream);
 }
 
-extern "C" int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, float* out, vqa_stream_t stream) {
-  VQA_ARG(x && out && rows > 0 && n > 0, "rowsum: bad arguments");
-  hipLaunchKernelGGL(rowsum_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, (long long)n, scale, out);
+extern "C" size_t vqa_rowsum_workspace(int64_t rows, int64_t n) {
+  return (size_t)rows * ((n + kRowsumChunk - 1) / kRowsumChunk) * sizeof(float);
+}
+
+extern "C" int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, float* out, void* workspace,
+                          size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(x && out && rows > 0 && n > 0 && rows < (1 << 20), "rowsum: bad arguments");
+  VQA_ARG(workspace && ws_bytes >= vqa_rowsum_workspace(rows, n), "rowsum: workspace too small");
+  const int nch = (int)((n + kRowsumChunk - 1) / kRowsumChunk);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(rowsum_part_kernel, dim3((unsigned)(rows * nch)), dim3(256), 0, s, x, (long long)n, nch,
+                     (float*)workspace);
+  hipLaunchKernelGGL(rowsum_final_kernel, dim3((unsigned)rows), dim3(256), 0, s, (const float*)workspace, nch, scale,
+                     out);
   VQA_LAUNCHED("rowsum_kernel");
   return VQA_OK;
 }
@@ -1564,7 +1596,7 @@ extern "C" int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const 
                                 int64_t* tokens, void* cache, size_t cache_bytes, int N, int steps, int ctx, int width,
                                 int heads, int blocks, int bins, int64_t start, uint64_t seed, vqa_stream_t stream) {
   VQA_ARG(layers && x_embedding && pos_embedding && out_kernel && out_bias && tokens && cache && N > 0 && steps > 0 &&
-              steps <= ctx && blocks > 0 && ctx % blocks == 0 && bins > 0 && bins <= 2048,
+              steps <= ctx && blocks > 0 && ctx % blocks == 0 && bins > 0 && bins <= 2048 && bins % 4 == 0,
           "prior_decode: bad arguments");
   VQA_REQUIRE(depth > 0 && depth <= kDecMaxLayers && width == kDecW && heads > 0 && kDecAW % heads == 0 &&
                   kDecAW / heads <= 32 && ctx / blocks <= kDecMaxL && heads <= 4,

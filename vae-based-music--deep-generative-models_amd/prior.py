@@ -179,11 +179,12 @@ class ResidualAttnBlock:
         V.attn_bwd(qh, kh, vh, oh, lse, doh, dsum, dqh, dkh, dvh, f.attn_func, f.block_len, f.num_heads,
                    1.0 / math.sqrt(f.head_dim))
         if f.attn_func == 2:
-            # the zero block of block 0: its values are the value bias, d(bias) += sum of dO over block 0
+            # the zero block of block 0: its values are the value bias, d(bias) += sum of dO over block 0 —
+            # per-position sums over the batch, then a fixed-order reduction of those rows (deferred)
             tmp = torch.empty(f.block_len, w, dtype=torch.float32, device=x.device)
             V.colsum(doh, tmp, N, T * w, f.block_len * w)
             extra = torch.empty(w, dtype=torch.float32, device=x.device)
-            V.colsum(tmp, extra, f.block_len, w, w)
+            deferred.add(V.PartialsDesc(tmp.data_ptr(), extra.data_ptr(), None, f.block_len, w, w, 0), tmp)
             post_adds.append((f.g("mha/value/bias").view(-1), extra))
         dqkv = torch.empty_like(qkv)
         for j, (n, dh) in enumerate((("query", dqh), ("key", dkh), ("value", dvh))):

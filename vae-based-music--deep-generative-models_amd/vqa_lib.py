@@ -38,7 +38,7 @@ EXPORTED = [
     "vqa_layernorm_bwd", "vqa_layernorm_bwd_workspace",
     "vqa_seqlin_fwd", "vqa_seqlin_wgrad_workspace", "vqa_seqlin_wgrad", "vqa_prior_embed_fwd", "vqa_colsum",
     "vqa_axpy", "vqa_dropout", "vqa_scale_f32", "vqa_tf_mix", "vqa_attn_fwd", "vqa_attn_bwd", "vqa_head_wt",
-    "vqa_head_fwd", "vqa_head_bwd_workspace", "vqa_head_bwd", "vqa_rowsum", "vqa_prior_decode_cache_bytes",
+    "vqa_head_fwd", "vqa_head_bwd_workspace", "vqa_head_bwd", "vqa_rowsum_workspace", "vqa_rowsum", "vqa_prior_decode_cache_bytes",
     "vqa_prior_decode",
 ]
 
@@ -129,7 +129,8 @@ _SIGS = {
     "vqa_head_fwd": (_I, [_P] * 8 + [_L, _I, _I, _I, _P]),
     "vqa_head_bwd_workspace": (_S, [_L, _I, _I]),
     "vqa_head_bwd": (_I, [_P] * 5 + [_F, _P, _P, _P, _L, _I, _I, _I, _P, _S, _P, _P]),
-    "vqa_rowsum": (_I, [_P, _L, _L, _F, _P, _P]),
+    "vqa_rowsum_workspace": (_S, [_L, _L]),
+    "vqa_rowsum": (_I, [_P, _L, _L, _F, _P, _P, _S, _P]),
     "vqa_prior_decode_cache_bytes": (_S, [_I, _I, _I]),
     "vqa_prior_decode": (_I, [_P, _I] + [_P] * 10 + [_S] + [_I] * 7 + [_L, _U, _P]),
 }
@@ -639,7 +640,8 @@ def head_bwd(x, wt, bias, targets, lse, inv_count, dx, dw, db, deferred=None):
 
 
 def rowsum(x, rows, n, scale, out):
-    _check(lib().vqa_rowsum(ptr(x), rows, n, scale, ptr(out), stream()), "vqa_rowsum")
+    ws = workspace(lib().vqa_rowsum_workspace(rows, n), x.device)
+    _check(lib().vqa_rowsum(ptr(x), rows, n, scale, ptr(out), ptr(ws), ws.numel(), stream()), "vqa_rowsum")
 
 
 class PriorLayerDesc(ctypes.Structure):
