@@ -278,6 +278,30 @@ __device__ __forceinline__ void load_wfrags(typename Mfma<T>::frag (&wf)[3][2][r
       }
 }
 
+// A fragments of a TRANSPOSED conv (output = Keras input channel, input = Keras output channel) held in
+// registers: the same lane -> channel map as load_wfrags, read from the kernel transposed (no LDS image)
+template <class T>
+__device__ __forceinline__ void load_wfrags_t(typename Mfma<T>::frag (&wf)[3][2][rs_ncc<T>()], const float* w) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kc = rs_kcol<T, true>(lane);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int s = 0; s < rs_ncc<T>(); ++s) {
+        const int o = 8 * rs_sig(m >> 2) + 4 * mt + (m & 3);
+        if constexpr (sizeof(T) == 2) {
+          // the 8 inputs are contiguous in the Keras kernel: two 16-byte loads
+          const f32x4* src = (const f32x4*)(w + (k * RC + o) * RC + s * 32 + kc);
+          const f32x4 lo = src[0], hi = src[1];
+          wf[k][mt][s] = bf16x8{(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
+                                (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+        } else {
+          wf[k][mt][s] = w[(k * RC + o) * RC + s * 4 + kc];
+        }
+      }
+}
+
 // NJ 16-row n-tiles at once: every B fragment is loaded before the first MFMA, then the MFMAs run tap-major
 // over the n-tiles (2*NJ independent accumulator chains), so the LDS latency and the MFMA dependency chain
 // are hidden inside the wave. Output acc[j][mt]: rows rb[j] + rs_pi(lane & 15), channels rs_ocol(lane) +
@@ -458,21 +482,20 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   constexpr int WS = rs_stride<T>(), XS = WS, NT = RT / 16, NJ = (NT + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int d = DT > 0 ? DT : a.d, HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
-  // conv_a's forward A fragments (recompute h) live in registers; the two transposed convs read LDS images
-  T* waT = (T*)smem;            // conv_a^T: output c, input o
-  T* wbT = waT + 3 * RC * WS;   // conv_b^T: output c, input o
-  T* X = wbT + 3 * RC * WS;     // local j <-> row t0 - 2d + j: relu(x)
+  // every weight operand lives in registers: conv_a's forward fragments (recompute h) and the two transposed
+  // convs' fragments (dh, dx)
+  T* X = (T*)smem;              // local j <-> row t0 - 2d + j: relu(x)
   T* Y = X + XR * XS;           // local m <-> row t0 - d - 1 + m (dy)
   T* H = Y + YR * XS;           // local i <-> row t0 - d + i: relu(h), then dh
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
             tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
-  typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()];
+  typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()], wta[3][2][rs_ncc<T>()], wtb[3][2][rs_ncc<T>()];
   load_wfrags<T, true>(wfa, a.wa);
-  stage_wimg<T, false>(waT, a.wa);
-  stage_wimg<T, false>(wbT, a.wb);
-  const int pn = rs_pi(lane & 15), oc = rs_ocol(lane), kc = rs_kcol<T, true>(lane);
+  load_wfrags_t<T>(wta, a.wa);
+  load_wfrags_t<T>(wtb, a.wb);
+  const int pn = rs_pi(lane & 15), oc = rs_ocol(lane);
   f32x4 bav[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) bav[mt] = a.ba ? bias4(a.ba, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -494,11 +517,6 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     const size_t o = item_off(tile);
     bx.load(rs_rsrc((const T*)a.x + o, ibytes), tstart(tile) - 2 * d);
     by.load(rs_rsrc((const T*)a.dy + o, ibytes), tstart(tile) - d - 1);
-  };
-  // A fragments from a weight image: lane reads row k*32 + mt*16 + pi(m), K slice kc
-  auto img_frag = [&](const T* img) {
-    const T* p = img + pn * WS + kc;
-    return [=](int k, int mt, int sc) { return M::load(p + (k * RC + mt * 16) * WS + sc * M::KS); };
   };
   Rows32Buf<T, rs_pv<T>()> nx, ny;
   nx.init(XR);
@@ -563,7 +581,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       int rb[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = rh[j] + 2;
-      conv_multi<T, false, true, true, 3>(dh, img_frag(wbT), Y, rb, -1);
+      conv_multi<T, false, true, false, 3>(dh, [&](int k, int mt, int sc) { return wtb[k][mt][sc]; }, Y, rb, -1);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if constexpr (sizeof(T) == 2) {
@@ -596,7 +614,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       f32x4 acc[NJ][2];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) rb[j] = min(wave + 4 * j, NT - 1) * 16 + 2 * d;
-      conv_multi<T, false, true, true, NJ>(acc, img_frag(waT), H, rb, -d);
+      conv_multi<T, false, true, false, NJ>(acc, [&](int k, int mt, int sc) { return wta[k][mt][sc]; }, H, rb, -d);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (wave + 4 * j >= NT) continue;
@@ -671,7 +689,7 @@ static size_t fwd_lds(int d, int esz, int rt) {
 }
 static size_t bwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = round16(rt + 2 * d);
-  return ((size_t)6 * RC * s + (size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
+  return ((size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
 }
 
 static int set_lds(const void* fn, size_t bytes) {
