@@ -121,6 +121,140 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* x, const T*
     part[(size_t)blockIdx.x * 2 * C + e] = ((red[e] + red[2 * C + e]) + red[4 * C + e]) + red[6 * C + e];
 }
 
+// Vectorised forms for C = 8R (R = lanes per row, a power of two <= 64): each lane owns 8 consecutive channels
+// (one 16-byte bf16 access), a wave holds 64/R rows at once, row statistics by R-lane butterflies (fixed order).
+template <int R>
+__device__ __forceinline__ float grp_sum_r(float v) {
+#pragma unroll
+  for (int o = R / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <class T> __device__ __forceinline__ void ld8v(const T* p, float (&v)[8]);
+template <> __device__ __forceinline__ void ld8v<bf16>(const bf16* p, float (&v)[8]) {
+  const bf16x8 b = *(const bf16x8*)p;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)b[i];
+}
+template <> __device__ __forceinline__ void ld8v<float>(const float* p, float (&v)[8]) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+template <class T> __device__ __forceinline__ void st8v(T* p, const float (&v)[8]);
+template <> __device__ __forceinline__ void st8v<bf16>(bf16* p, const float (&v)[8]) {
+  bf16x8 b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (bf16)v[i];
+  *(bf16x8*)p = b;
+}
+template <> __device__ __forceinline__ void st8v<float>(float* p, const float (&v)[8]) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+template <class T, int R>
+__global__ __launch_bounds__(256) void layernorm8_fwd_kernel(const T* x, const float* gamma, const float* beta, T* y,
+                                                            long long rows, float eps) {
+  constexpr int C = 8 * R, RPW = 64 / R;
+  const int lane = threadIdx.x & 63, sub = lane / R, c0 = 8 * (lane % R);
+  float gm[8], bt[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { gm[i] = gamma[c0 + i]; bt[i] = beta[c0 + i]; }
+  const long long rstep = (long long)gridDim.x * 4 * RPW;
+  for (long long r = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub; r < rows; r += rstep) {
+    float v[8];
+    ld8v(x + r * C + c0, v);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+    const float mean = grp_sum_r<R>(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
+    const float inv = 1.0f / sqrtf(grp_sum_r<R>(q) / (float)C + eps);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (v[i] - mean) * inv * gm[i] + bt[i];
+    st8v(y + r * C + c0, v);
+  }
+}
+
+template <class T, int R>
+__global__ __launch_bounds__(256) void layernorm8_bwd_kernel(const T* x, const T* dy, const float* gamma, T* dx,
+                                                            float* part, long long rows, float eps,
+                                                            long long rows_per_wg) {
+  constexpr int C = 8 * R, RPW = 64 / R;
+  extern __shared__ float red[];  // [4][2C]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane / R, c0 = 8 * (lane % R);
+  float gm[8], gg[8], gb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { gm[i] = gamma[c0 + i]; gg[i] = gb[i] = 0.f; }
+  const long long r0 = (long long)blockIdx.x * rows_per_wg, r1 = std::min(rows, r0 + rows_per_wg);
+  for (long long r = r0 + wave * RPW + sub; r < r1; r += 4 * RPW) {
+    float v[8], d[8];
+    ld8v(x + r * C + c0, v);
+    ld8v(dy + r * C + c0, d);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+    const float mean = grp_sum_r<R>(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
+    const float inv = 1.0f / sqrtf(grp_sum_r<R>(q) / (float)C + eps);
+    float g[8], sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      v[i] = (v[i] - mean) * inv;  // xhat
+      g[i] = d[i] * gm[i];
+      sg += g[i];
+      sgx += g[i] * v[i];
+      gg[i] += d[i] * v[i];
+      gb[i] += d[i];
+    }
+    const float mg = grp_sum_r<R>(sg) / (float)C, mgx = grp_sum_r<R>(sgx) / (float)C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = inv * ((g[i] - mg) - v[i] * mgx);
+    st8v(dx + r * C + c0, g);
+  }
+  // combine the wave's row groups (lanes with the same channels: xor R, 2R, ...), then the 4 waves in order
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int o = R; o < 64; o <<= 1) {
+      gg[i] += __shfl_xor(gg[i], o, 64);
+      gb[i] += __shfl_xor(gb[i], o, 64);
+    }
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[wave * 2 * C + c0 + i] = gg[i];
+      red[wave * 2 * C + C + c0 + i] = gb[i];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * C; e += 256)
+    part[(size_t)blockIdx.x * 2 * C + e] = ((red[e] + red[2 * C + e]) + red[4 * C + e]) + red[6 * C + e];
+}
+
+template <class T, int R>
+static int launch_ln8(bool fwd, const void* x, const void* dy, const float* gamma, const float* beta, void* out,
+                      float* part, long long rows, float eps, int nwg, hipStream_t s) {
+  constexpr int C = 8 * R, RPW = 64 / R;
+  if (fwd) {
+    const unsigned g = (unsigned)std::min<long long>((rows + 4 * RPW - 1) / (4 * RPW), 2048);
+    hipLaunchKernelGGL((layernorm8_fwd_kernel<T, R>), dim3(g), dim3(256), 0, s, (const T*)x, gamma, beta, (T*)out,
+                       rows, eps);
+    VQA_LAUNCHED("layernorm8_fwd_kernel");
+  } else {
+    const long long rpw = (rows + nwg - 1) / nwg;
+    hipLaunchKernelGGL((layernorm8_bwd_kernel<T, R>), dim3(nwg), dim3(256), (size_t)8 * C * sizeof(float), s,
+                       (const T*)x, (const T*)dy, gamma, (T*)out, part, rows, eps, rpw);
+    VQA_LAUNCHED("layernorm8_bwd_kernel");
+  }
+  return VQA_OK;
+}
+
 static int ln_wgs(long long rows) {
   long long w = (rows + 63) / 64;  // >= 16 rows per wave
   return (int)std::max<long long>(1, std::min<long long>(w, 512));
@@ -146,6 +280,9 @@ static int launch_ln(bool fwd, const void* x, const void* dy, const float* gamma
 template <class T>
 static int dispatch_ln(bool fwd, const void* x, const void* dy, const float* gamma, const float* beta, void* out,
                        float* part, long long rows, int C, float eps, int nwg, hipStream_t s) {
+  if (C == 128) return launch_ln8<T, 16>(fwd, x, dy, gamma, beta, out, part, rows, eps, nwg, s);
+  if (C == 256) return launch_ln8<T, 32>(fwd, x, dy, gamma, beta, out, part, rows, eps, nwg, s);
+  if (C == 64) return launch_ln8<T, 8>(fwd, x, dy, gamma, beta, out, part, rows, eps, nwg, s);
   const int lc = (C + 63) / 64;
   if (lc <= 1) return launch_ln<T, 1>(fwd, x, dy, gamma, beta, out, part, rows, C, eps, nwg, s);
   if (lc <= 2) return launch_ln<T, 2>(fwd, x, dy, gamma, beta, out, part, rows, C, eps, nwg, s);

@@ -102,11 +102,17 @@ __global__ __launch_bounds__(256) void seqlin_kernel(SeqLinArgs a) {
   for (int tap = 0; tap < a.taps; ++tap) {
     if (tap) __syncthreads();  // every read of the previous tap's weights is done
     const float* w = a.w + (size_t)tap * a.K * a.N;
-    for (int e = threadIdx.x; e < a.K * a.N; e += 256) {
-      int n, k;
-      if (a.wtrans) { n = e / a.K; k = e - n * a.K; }
-      else { k = e / a.N; n = e - k * a.N; }
-      Wt[n * KS + k] = (T)w[e];
+    // 16-byte coalesced weight reads (4 consecutive elements of the contiguous axis)
+    for (int e4 = threadIdx.x; e4 < a.K * a.N / 4; e4 += 256) {
+      const f32x4 v = *(const f32x4*)(w + 4 * e4);
+      if (a.wtrans) {  // w[n][k]: 4 consecutive k of one n
+        const int n = 4 * e4 / a.K, k = 4 * e4 - n * a.K;
+        st4(Wt + n * KS + k, v);
+      } else {         // w[k][n]: 4 consecutive n of one k
+        const int k = 4 * e4 / a.N, n = 4 * e4 - k * a.N;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Wt[(n + i) * KS + k] = (T)v[i];
+      }
     }
     __syncthreads();
     // row j of X for output row i: i + dir * (taps - 1 - tap) + lo
@@ -1317,6 +1323,7 @@ extern "C" int vqa_seqlin_fwd(const void* x, int64_t ldx, const float* w, const 
               VQA_E_UNSUPPORTED, "seqlin_fwd: K=%d N=%d unsupported", K, N);
   VQA_ARG(ldx % vec == 0 && ldy % 4 == 0 && (!residual || ldr % 4 == 0) && ldx >= K && ldy >= N,
           "seqlin_fwd: strides must keep 16-byte rows");
+  VQA_ARG(((uintptr_t)w & 15) == 0, "seqlin_fwd: weights must be 16-byte aligned");
   SeqLinArgs a{x, w, bias, residual, y, ldx, ldr, ldy, nseq, T, K, N, taps, dir, wtrans, accumulate,
                (T + kSlRows - 1) / kSlRows};
   hipStream_t s = (hipStream_t)stream;
