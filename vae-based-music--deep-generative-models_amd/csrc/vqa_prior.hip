@@ -1046,6 +1046,9 @@ constexpr int kDecMaxL = 2048;
 struct DecLayer {
   const float *ln1g, *ln1b, *qkvw, *qkvb, *qw, *qb, *kw, *kb, *vw, *vb, *ow, *ob, *pw, *pb, *ln2g, *ln2b, *mw, *mb;
   int type;
+  // composed once per decode (prior_decode_prep_kernel): the causal conv followed by the query/key/value
+  // EinsumDense (one 384 x 96 map straight to the heads) and the output EinsumDense followed by proj (32 x 128)
+  float *cw, *cb, *opw, *opb;
 };
 
 struct DecArgs {
@@ -1113,11 +1116,45 @@ __device__ void dec_layernorm(const float* x, const float* gm, const float* bt, 
   __syncthreads();
 }
 
+// Linear maps of a layer composed in fp32 (the decode step then does 3 mat-vecs per layer instead of 7):
+//   cw[tap*128 + k][j*32 + n] = sum_m qkvw[tap][k][j*32 + m] * Wj[m][n]   (j = query, key, value)
+//   cb[j*32 + n] = sum_m qkvb[j*32 + m] * Wj[m][n] + bj[n]
+//   opw[k][n] = sum_m ow[k][m] * pw[m][n],  opb[n] = sum_m ob[m] * pw[m][n] + pb[n]
+__global__ __launch_bounds__(256) void prior_decode_prep_kernel(DecArgs a) {
+  const DecLayer& ly = a.L[blockIdx.y];
+  const int nc = 3 * kDecW * 3 * kDecAW, nb = 3 * kDecAW, no = kDecAW * kDecW;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nc + nb + no + kDecW; e += gridDim.x * 256) {
+    if (e < nc) {
+      const int row = e / (3 * kDecAW), col = e - row * (3 * kDecAW), j = col / kDecAW, n = col - j * kDecAW;
+      const float* Wj = j == 0 ? ly.qw : j == 1 ? ly.kw : ly.vw;
+      float s = 0.f;
+      for (int m = 0; m < kDecAW; ++m) s += ly.qkvw[row * 3 * kDecAW + j * kDecAW + m] * Wj[m * kDecAW + n];
+      ly.cw[e] = s;
+    } else if (e < nc + nb) {
+      const int col = e - nc, j = col / kDecAW, n = col - j * kDecAW;
+      const float* Wj = j == 0 ? ly.qw : j == 1 ? ly.kw : ly.vw;
+      const float* bj = j == 0 ? ly.qb : j == 1 ? ly.kb : ly.vb;
+      float s = 0.f;
+      for (int m = 0; m < kDecAW; ++m) s += ly.qkvb[j * kDecAW + m] * Wj[m * kDecAW + n];
+      ly.cb[col] = s + bj[n];
+    } else if (e < nc + nb + no) {
+      const int q = e - nc - nb, k = q / kDecW, n = q - k * kDecW;
+      float s = 0.f;
+      for (int m = 0; m < kDecAW; ++m) s += ly.ow[k * kDecAW + m] * ly.pw[m * kDecW + n];
+      ly.opw[q] = s;
+    } else {
+      const int n = e - nc - nb - no;
+      float s = 0.f;
+      for (int m = 0; m < kDecAW; ++m) s += ly.ob[m] * ly.pw[m * kDecW + n];
+      ly.opb[n] = s + ly.pb[n];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
   __shared__ __attribute__((aligned(16))) float x[kDecW], x1[kDecW], hb[kDecW], r1[kDecW];
   __shared__ float ring[kDecMaxLayers][3][kDecW];
-  __shared__ __attribute__((aligned(16))) float cat[3 * kDecW], qkv[3 * kDecAW], qh[kDecAW], kh[kDecAW], vh[kDecAW],
-      oh[kDecAW], o32[kDecAW];
+  __shared__ __attribute__((aligned(16))) float cat[3 * kDecW], qkv[3 * kDecAW], oh[kDecAW];
   __shared__ float sc[2][kDecMaxL];
   __shared__ __attribute__((aligned(16))) float scr[2048];
   __shared__ __attribute__((aligned(16))) float red[32][kDecAW];
@@ -1154,10 +1191,10 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
         }
       }
       __syncthreads();
-      dec_matvec(cat, 3 * kDecW, ly.qkvw, ly.qkvb, qkv, 3 * kDecAW, scr);
-      dec_matvec(qkv, kDecAW, ly.qw, ly.qb, qh, kDecAW, scr);
-      dec_matvec(qkv + kDecAW, kDecAW, ly.kw, ly.kb, kh, kDecAW, scr);
-      dec_matvec(qkv + 2 * kDecAW, kDecAW, ly.vw, ly.vb, vh, kDecAW, scr);
+      dec_matvec(cat, 3 * kDecW, ly.cw, ly.cb, qkv, 3 * kDecAW, scr);  // [q heads | k heads | v heads]
+      const float* qh = qkv;
+      const float* kh = qkv + kDecAW;
+      const float* vh = qkv + 2 * kDecAW;
       float* kcL = a.kc + (((size_t)n * a.depth + L) * a.T) * kDecAW;
       float* vcL = a.vc + (((size_t)n * a.depth + L) * a.T) * kDecAW;
       if (tid < kDecAW) {
@@ -1177,10 +1214,17 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
       } else {
         const int hd = kDecAW / a.H;
         for (int idx = tid; idx < cnt; idx += 256) {
-          const float* kr = kcL + (size_t)(j0 + idx * jstep) * kDecAW;
+          const f32x4* kr = (const f32x4*)(kcL + (size_t)(j0 + idx * jstep) * kDecAW);
+          const f32x4* qv = (const f32x4*)qh;
+          f32x4 kv[kDecAW / 4];
+#pragma unroll
+          for (int c = 0; c < kDecAW / 4; ++c) kv[c] = kr[c];
           for (int h = 0; h < a.H; ++h) {
             float s = 0.f;
-            for (int d = 0; d < hd; ++d) s += qh[h * hd + d] * kr[h * hd + d];
+            for (int c = h * hd / 4; c < (h + 1) * hd / 4; ++c) {
+              const f32x4 pq = qv[c] * kv[c];
+              s += (pq[0] + pq[1]) + (pq[2] + pq[3]);
+            }
             sc[h][idx] = s * a.scale;
           }
         }
@@ -1219,8 +1263,7 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
         }
         __syncthreads();
       }
-      dec_matvec(oh, kDecAW, ly.ow, ly.ob, o32, kDecAW, scr);
-      dec_matvec(o32, kDecAW, ly.pw, ly.pb, r1, kDecW, scr);
+      dec_matvec(oh, kDecAW, ly.opw, ly.opb, r1, kDecW, scr);  // output EinsumDense o proj
       if (tid < kDecW) x1[tid] = x[tid] + r1[tid];
       __syncthreads();
       dec_layernorm(x1, ly.ln2g, ly.ln2b, hb, a.eps, stat);
@@ -1593,8 +1636,10 @@ extern "C" int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, 
   return VQA_OK;
 }
 
+constexpr size_t kDecComposed = (size_t)3 * kDecW * 3 * kDecAW + 3 * kDecAW + kDecAW * kDecW + kDecW;  // floats/layer
+
 extern "C" size_t vqa_prior_decode_cache_bytes(int N, int depth, int ctx) {
-  return (size_t)2 * N * depth * ctx * kDecAW * sizeof(float);
+  return ((size_t)2 * N * depth * ctx * kDecAW + (size_t)depth * kDecComposed) * sizeof(float);
 }
 
 extern "C" int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const float* x_embedding,
@@ -1611,12 +1656,16 @@ extern "C" int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const 
               ctx / blocks);
   VQA_ARG(cache_bytes >= vqa_prior_decode_cache_bytes(N, depth, ctx), "prior_decode: cache too small");
   DecArgs a;
+  float* comp = (float*)cache + (size_t)2 * N * depth * ctx * kDecAW;
   for (int L = 0; L < depth; ++L) {
     const vqa_prior_layer& s = layers[L];
     VQA_ARG(s.attn_type >= 0 && s.attn_type <= 2, "prior_decode: layer %d attention type %d", L, s.attn_type);
+    float* c = comp + (size_t)L * kDecComposed;
     a.L[L] = DecLayer{s.ln1_gamma, s.ln1_beta, s.qkv_kernel, s.qkv_bias, s.query_kernel, s.query_bias, s.key_kernel,
                       s.key_bias, s.value_kernel, s.value_bias, s.out_kernel, s.out_bias, s.proj_kernel, s.proj_bias,
-                      s.ln2_gamma, s.ln2_beta, s.mlp_kernel, s.mlp_bias, s.attn_type};
+                      s.ln2_gamma, s.ln2_beta, s.mlp_kernel, s.mlp_bias, s.attn_type,
+                      c, c + 3 * kDecW * 3 * kDecAW, c + 3 * kDecW * 3 * kDecAW + 3 * kDecAW,
+                      c + 3 * kDecW * 3 * kDecAW + 3 * kDecAW + kDecAW * kDecW};
   }
   a.emb = x_embedding; a.pos = pos_embedding; a.hw = out_kernel; a.hb = out_bias;
   a.ycond = ycond; a.xcond = xcond; a.forced = forced; a.logits = logits; a.tokens = tokens;
@@ -1627,6 +1676,8 @@ extern "C" int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const 
   a.scale = 1.0f / sqrtf((float)(kDecAW / heads));
   a.emb_scale = sqrtf((float)width);
   a.eps = 1e-6f;
+  hipLaunchKernelGGL(prior_decode_prep_kernel, dim3(64, depth), dim3(256), 0, (hipStream_t)stream, a);
+  VQA_LAUNCHED("prior_decode_prep_kernel");
   hipLaunchKernelGGL(prior_decode_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, a);
   VQA_LAUNCHED("prior_decode_kernel");
   return VQA_OK;
