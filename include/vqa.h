@@ -308,10 +308,12 @@ int vqa_dropout(void* x, int64_t n, float rate, uint64_t seed, uint64_t salt, co
                 vqa_stream_t stream);
 int vqa_scale_f32(float* x, int64_t n, float s, vqa_stream_t stream);
 /* prior.py:262-290 teacher forcing: latent = [start, codes[:-1]]; pred = [start, amax[:-1]];
- * out = m ? pred : latent, m = mask[r] (uint8, when given) or uniform(seed, step + *counter, r) < rate; amax
- * NULL: out = latent. */
+ * out = m ? pred : latent, m = mask[r] (uint8, when given) or uniform(seed, step + *counter, row_offset + r)
+ * < rate (row_offset: the rank's first row of the global batch under data parallelism); amax NULL: out =
+ * latent. */
 int vqa_tf_mix(const int64_t* codes, const int64_t* amax, const uint8_t* mask, int64_t* out, int N, int T,
-               int64_t start, float rate, uint64_t seed, uint64_t step, const int64_t* counter, vqa_stream_t stream);
+               int64_t start, float rate, uint64_t seed, uint64_t step, int64_t row_offset, const int64_t* counter,
+               vqa_stream_t stream);
 /* Factorized attention core of keras MultiHeadAttention (softmax(q k^T * scale + mask) v per head) on the
  * projected q, k, v (N, T, H*head_dim), head_dim 16. mode 0 row (causal within blocks of l,
  * factorized_attention.py:74-141), 1 col (causal over blocks at a fixed position, :210-286), 2 prev-row

@@ -1,0 +1,68 @@
+"""One rank of the prior's data-parallel test (tests/test_gpu_prior_dp.py; not collected by pytest).
+
+Runs Prior.train_step with a torch.distributed process group (gloo, every rank on cuda:0) on its shard of the
+global batch — eager, or as two captured hipGraphs around the eager all_reduce — and saves the state.
+    python tests/prior_dp_worker.py MODE OUT   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"), ROOT]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+N_LOCAL = 1
+
+
+def cfg():
+    from oracle import prior_ref as P
+    return P.PriorConfig(bins=64, ctx=256, width=128, depth=3, heads=2, blocks=4, attn_stacks=1)
+
+
+def build(process_group=None):
+    from oracle import prior_ref as P
+    from prior import Prior
+    c = cfg()
+    pr = Prior(0, [(c.ctx,)], c.bins, [3], [2], None,
+               dict(width=c.width, depth=c.depth, heads=c.heads, blocks=c.blocks, attn_stacks=c.attn_stacks,
+                    drop_out_rate=0.0), None, dtype="fp32", device="cuda:0", seed=3, process_group=process_group)
+    pr.prior.store.set_values(P.init_params(c, 3))
+    return pr
+
+
+def batches(world):
+    c = cfg()
+    g = torch.Generator().manual_seed(17)
+    return [torch.randint(0, c.bins - 1, (N_LOCAL * world, c.ctx), generator=g) for _ in range(2)]
+
+
+def snapshot(pr):
+    st = pr.prior.store
+    return {"weights": st.flat.detach().cpu().clone(), "grads": st.grad[:st.size].detach().cpu().clone(),
+            "adam_m": pr.optimizer.m.cpu().clone(), "loss": float(pr.results()["loss"]),
+            "accuracy": float(pr.results()["accuracy"]), "batch_input": pr._last_batch_input.cpu().clone()}
+
+
+def main():
+    mode, out = sys.argv[1], sys.argv[2]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pr = build()
+    xs = [x[rank * N_LOCAL:(rank + 1) * N_LOCAL].cuda() for x in batches(world)]
+    if mode == "eager":
+        pr.train_step(xs[0])
+        pr.train_step(xs[1])
+    else:  # one eager warm-up step on xs[0] (inside capture), then the captured step replayed on xs[1]
+        pr.capture_train_step(xs[0], warmup=1)
+        pr.train_step(xs[1])
+    torch.cuda.synchronize()
+    torch.save(snapshot(pr), out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

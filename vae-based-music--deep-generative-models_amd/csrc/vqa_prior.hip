@@ -335,13 +335,13 @@ __global__ __launch_bounds__(256) void scale_f32_kernel(float* x, long long n, f
 __global__ __launch_bounds__(256) void tf_mix_kernel(const int64_t* codes, const int64_t* amax, const uint8_t* mask,
                                                     int64_t* out, long long rows, int T, int64_t start, float rate,
                                                     unsigned long long seed, unsigned long long step0,
-                                                    const int64_t* ctr) {
+                                                    long long row_offset, const int64_t* ctr) {
   const unsigned long long step = step0 + (ctr ? (unsigned long long)*ctr : 0ull);
   for (long long r = (long long)blockIdx.x * 256 + threadIdx.x; r < rows; r += (long long)gridDim.x * 256) {
     const int t = (int)(r % T);
     const int64_t latent = t == 0 ? start : codes[r - 1];
     bool m = false;
-    if (amax) m = mask ? mask[r] != 0 : prior_uniform(seed, 0x5446ull, step, (uint64_t)r) < rate;
+    if (amax) m = mask ? mask[r] != 0 : prior_uniform(seed, 0x5446ull, step, (uint64_t)(r + row_offset)) < rate;
     out[r] = m ? (t == 0 ? start : amax[r - 1]) : latent;
   }
 }
@@ -1473,12 +1473,12 @@ extern "C" int vqa_scale_f32(float* x, int64_t n, float s, vqa_stream_t stream) 
 }
 
 extern "C" int vqa_tf_mix(const int64_t* codes, const int64_t* amax, const uint8_t* mask, int64_t* out, int N, int T,
-                          int64_t start, float rate, uint64_t seed, uint64_t step, const int64_t* counter,
-                          vqa_stream_t stream) {
+                          int64_t start, float rate, uint64_t seed, uint64_t step, int64_t row_offset,
+                          const int64_t* counter, vqa_stream_t stream) {
   VQA_ARG(codes && out && N > 0 && T > 0 && (!mask || amax), "tf_mix: bad arguments");
   const long long rows = (long long)N * T;
   hipLaunchKernelGGL(tf_mix_kernel, dim3(pr_grid(rows)), dim3(256), 0, (hipStream_t)stream, codes, amax, mask, out,
-                     rows, T, start, rate, (unsigned long long)seed, (unsigned long long)step, counter);
+                     rows, T, start, rate, (unsigned long long)seed, (unsigned long long)step, (long long)row_offset, counter);
   VQA_LAUNCHED("tf_mix_kernel");
   return VQA_OK;
 }

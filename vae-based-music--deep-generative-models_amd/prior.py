@@ -30,6 +30,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+import vqa_dp
 import vqa_lib as V
 from conditioners import ConditionerNet
 from vqa_layers import ParamStore
@@ -246,7 +247,7 @@ class FMHABasedAutoregressiveModel:
     def __init__(self, target_vocab_size, width, depth, blocks, m_attn=0.25, m_mlp=1.0, heads=1, attn_stacks=1,
                  maximum_pos_encoding=5000, drop_out_rate=0.1, context_length=None, zq_shapes=None, level=0, levels=3,
                  pos_emb=True, downs=None, strides=None, cond_kwargs=None, dtype="fp32", device="cuda", seed=1,
-                 store: Optional[ParamStore] = None, prefix="prior", **kwargs):
+                 store: Optional[ParamStore] = None, prefix="prior", grad_extra: int = 0, **kwargs):
         self.context_length = int(np.prod(context_length))
         self.bins, self.d_model, self.depth = target_vocab_size, width, depth
         self.heads, self.blocks = heads, blocks
@@ -278,7 +279,8 @@ class FMHABasedAutoregressiveModel:
         if self.conditioner is not None:
             self.conditioner.build(st, f"{prefix}/conditioner", width, self.cdt)
         if own:
-            st.materialize(self.device, seed=seed)
+            # the gradient buffer is the head of the data-parallel bucket: grad_extra trailing slots for scalars
+            st.materialize(self.device, grad_buffer=torch.zeros(st.size + grad_extra, device=self.device), seed=seed)
         self._pos_table = None
         if not pos_emb:
             self._pos_table = torch.from_numpy(positional_encoding(maximum_pos_encoding, width)[0]).to(self.device)
@@ -391,7 +393,7 @@ class Prior:
 
     def __init__(self, level, z_shapes, bins, down_depth, strides, vqvae_model, prior_kwargs, x_cond_kwargs,
                  prior_monitor=None, genre_classes=None, dtype="fp32", device="cuda", seed=1, learning_rate=1e-3,
-                 **kwargs):
+                 process_group=None, **kwargs):
         assert len(down_depth) == len(strides) == len(z_shapes)
         self.level, self.z_shapes, self.levels = level, z_shapes, len(z_shapes)
         self.z_shape = z_shapes[level]
@@ -404,7 +406,12 @@ class Prior:
             heads=prior_kwargs["heads"], blocks=prior_kwargs["blocks"], attn_stacks=prior_kwargs["attn_stacks"],
             drop_out_rate=prior_kwargs.get("drop_out_rate", 0.1), context_length=self.z_shape, zq_shapes=z_shapes,
             level=level, levels=self.levels, downs=down_depth, strides=strides, cond_kwargs=x_cond_kwargs,
-            dtype=dtype, device=device, seed=seed)
+            dtype=dtype, device=device, seed=seed, grad_extra=2)
+        # data parallel (one process per GPU): ONE all_reduce per step over [gradients | loss, accuracy]
+        self.process_group = process_group
+        st = self.prior.store
+        self.bucket = st.grad
+        self._scalars = self.bucket[st.size:st.size + 2]
         self.label_conditioner = None
         if genre_classes is not None:
             raise NotImplementedError("label-conditioned training (LabelConditioner) is not built yet; the sampler "
@@ -417,7 +424,6 @@ class Prior:
         self.teacher_seed = 3
         self._step = 0
         self._graph = None
-        self._scalars = torch.zeros(2, dtype=torch.float32, device=self.device)
 
     @property
     def metrics(self):
@@ -453,13 +459,18 @@ class Prior:
         return {"loss": loss, "perplexity(per word)": torch.exp(loss), "accuracy": self.train_accuracy_tracker.result()}
 
     # -------------------------------------------------------------- the step
-    def _compute(self, codes, upper, teacher_force_rate, tf_mask=None, apply=True):
+    def _world(self):
+        return vqa_dp.world_size(self.process_group)
+
+    def _compute(self, codes, upper, teacher_force_rate, tf_mask=None):
+        """Both teacher-forcing passes and the backward: gradients and [loss, accuracy] sums in the bucket."""
         m, st = self.prior, self.prior.store
         N, T = codes.shape
         M = N * T
         dev = self.device
         seed = self.teacher_seed
         ctr = self.optimizer.iterations
+        row_offset = vqa_dp.rank(self.process_group) * M
         xc = m._cond(upper, save=True) if upper is not None else None
         # pass 1: teacher-forced input, argmax of the logits (prior.py:277-282)
         latent = torch.empty_like(codes)
@@ -476,7 +487,7 @@ class Prior:
         batch_input = torch.empty_like(codes)
         mask = None if tf_mask is None else torch.as_tensor(tf_mask, device=dev).to(torch.uint8).contiguous()
         V.tf_mix(codes, amax, mask, batch_input, m.start_token, rate=float(teacher_force_rate), seed=seed,
-                 counter=ctr)
+                 counter=ctr, row_offset=row_offset)
         h = m.hidden(batch_input, True, xc, save=True, seed=seed * 7919 + 2, counter=ctr)
         lse = torch.empty(M, dtype=torch.float32, device=dev)
         loss_row = torch.empty(M, dtype=torch.float32, device=dev)
@@ -485,8 +496,6 @@ class Prior:
         V.rowsum(loss_row, 1, M, 1.0 / M, self._scalars[0:1])
         V.rowsum(correct, 1, M, 1.0 / M, self._scalars[1:2])
         self._last_batch_input = batch_input
-        if not apply:
-            return
         deferred = V.Deferred()
         st.deferred = deferred
         post = []
@@ -512,22 +521,32 @@ class Prior:
             st.deferred = None
         if m.use_pos_embedding and T < m.context_length:
             st.grad_view(m.pos_name)[T:].zero_()
-        self.optimizer.apply(st)
 
-    def _update_metrics(self):
-        self.train_loss_tracker.update_state(self._scalars[0])
-        self.train_accuracy_tracker.update_state(self._scalars[1])
+    def _exchange(self):
+        vqa_dp.exchange(self.bucket, self.process_group)
+
+    def _apply(self):
+        """Keras Adam on the (rank-mean) gradients, then the trackers on the global means."""
+        w = self._world()
+        self.optimizer.apply(self.prior.store, grad_scale=1.0 / w)
+        self.train_loss_tracker.update_state(self._scalars[0] / w)
+        self.train_accuracy_tracker.update_state(self._scalars[1] / w)
 
     def train_step(self, x, teacher_force_rate=0.2, tf_mask=None):
         """prior.py:241-335. tf_mask (N, T) bool overrides the random teacher-forcing draw (parity tests)."""
         codes, upper = self._codes(x)
         if self._graph is not None and tf_mask is None and codes.shape == self._graph_codes.shape:
             self._graph_codes.copy_(codes)
-            self._graph.replay()
+            g1, g2 = self._graph
+            g1.replay()
+            if g2 is not None:
+                self._exchange()
+                g2.replay()
             self._step += 1
             return self.results()
         self._compute(codes, upper, teacher_force_rate, tf_mask)
-        self._update_metrics()
+        self._exchange()
+        self._apply()
         self._step += 1
         return self.results()
 
@@ -550,8 +569,9 @@ class Prior:
         return {"loss": out[0], "perplexity(per word)": torch.exp(out[0]), "accuracy": out[1]}
 
     def capture_train_step(self, codes_example, teacher_force_rate=0.2, warmup=1):
-        """Record the whole step (both passes, backward, Adam, metrics) as one hipGraph; later train_step calls
-        with this shape copy the codes in and replay (the teacher-forcing draw advances on the device)."""
+        """Record the whole step (both passes, backward, Adam, metrics) as one hipGraph — two around the eager
+        all_reduce under data parallelism; later train_step calls with this shape copy the codes in and replay
+        (the teacher-forcing draw advances on the device)."""
         codes, upper = self._codes(codes_example)
         if upper is not None:
             raise NotImplementedError("graph capture of the conditioned prior step")
@@ -561,14 +581,22 @@ class Prior:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._compute(self._graph_codes, None, teacher_force_rate)
-                self._update_metrics()
+                self._exchange()
+                self._apply()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        pool = torch.cuda.graph_pool_handle()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=pool):
             self._compute(self._graph_codes, None, teacher_force_rate)
-            self._update_metrics()
-        self._graph = g
+            if self._world() == 1:
+                self._apply()
+        g2 = None
+        if self._world() > 1:  # two graphs around the eager all_reduce
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool):
+                self._apply()
+        self._graph = (g1, g2)
         torch.cuda.synchronize(self.device)
 
     def sample(self, n_samples, z_cond=None, y=None, return_attn_weights=False, seed=0):

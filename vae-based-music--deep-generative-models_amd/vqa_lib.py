@@ -122,7 +122,7 @@ _SIGS = {
     "vqa_axpy": (_I, [_P, _P, _P, _L, _I, _P]),
     "vqa_dropout": (_I, [_P, _L, _F, _U, _U, _P, _I, _P]),
     "vqa_scale_f32": (_I, [_P, _L, _F, _P]),
-    "vqa_tf_mix": (_I, [_P, _P, _P, _P, _I, _I, _L, _F, _U, _U, _P, _P]),
+    "vqa_tf_mix": (_I, [_P, _P, _P, _P, _I, _I, _L, _F, _U, _U, _L, _P, _P]),
     "vqa_attn_fwd": (_I, [_P] * 6 + [_I] * 6 + [_F, _I, _P]),
     "vqa_attn_bwd": (_I, [_P] * 10 + [_I] * 6 + [_F, _I, _P]),
     "vqa_head_wt": (_I, [_P, _P, _I, _I, _I, _P]),
@@ -595,10 +595,10 @@ def scale_f32_(x, s):
     _check(lib().vqa_scale_f32(ptr(x), x.numel(), s, stream()), "vqa_scale_f32")
 
 
-def tf_mix(codes, amax, mask, out, start, rate=0.0, seed=0, step=0, counter=None):
+def tf_mix(codes, amax, mask, out, start, rate=0.0, seed=0, step=0, counter=None, row_offset=0):
     N, T = codes.shape
-    _check(lib().vqa_tf_mix(ptr(codes), ptr(amax), ptr(mask), ptr(out), N, T, start, rate, seed, step, ptr(counter),
-                            stream()), "vqa_tf_mix")
+    _check(lib().vqa_tf_mix(ptr(codes), ptr(amax), ptr(mask), ptr(out), N, T, start, rate, seed, step, row_offset,
+                            ptr(counter), stream()), "vqa_tf_mix")
 
 
 def attn_fwd(q, k, v, o, lse, mode, l, heads, scale, vbias=None):
