@@ -286,6 +286,18 @@ int vqa_stft_magnitude(const float* x, float* mag, int B, int T, int n_fft, int 
 int vqa_seqlin_fwd(const void* x, int64_t ldx, const float* w, const float* bias, const void* residual, int64_t ldr,
                    void* y, int64_t ldy, int nseq, int T, int K, int N, int taps, int dir, int wtrans, int accumulate,
                    int dtype, vqa_stream_t stream);
+/* The same layer with weights prepared once per step by vqa_seqlin_prep: wp = Wv laid out [taps][N][K] in the
+ * activation dtype (the kernel stages it with plain 16-byte copies). vqa_seqlin_prep converts a batch of
+ * layers in one launch: out[tap][n][k] = wtrans ? w[(tap*N + n)*K + k] : w[(tap*K + k)*N + n]. */
+typedef struct {
+  const float* w;
+  void* out;
+  int taps, K, N, wtrans;
+} vqa_seqlin_prep_desc;
+int vqa_seqlin_prep(const vqa_seqlin_prep_desc* descs, int count, int dtype, vqa_stream_t stream);
+int vqa_seqlin_fwd_prepped(const void* x, int64_t ldx, const void* wp, const float* bias, const void* residual,
+                           int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K, int N, int taps, int dir,
+                           int accumulate, int dtype, vqa_stream_t stream);
 /* dW[tap][k][n] = sum_t x[t-(taps-1-tap)][k] dy[t][n], db = sum_t dy[t] (deterministic partials; desc != NULL
  * defers the reduction as for the conv weight gradients). K <= 128, N <= 128, multiples of 16. */
 size_t vqa_seqlin_wgrad_workspace(int nseq, int T, int K, int N, int taps);

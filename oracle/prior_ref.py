@@ -264,7 +264,7 @@ def train_step_grads(p, cfg: PriorConfig, codes, tf_mask, prefix="prior", x_cond
     loss = ce_loss(codes, logits)
     loss.backward()
     grads = {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in leaves.items()}
-    return float(loss), float(accuracy(codes, logits.detach())), grads, batch_input
+    return float(loss.detach()), float(accuracy(codes, logits.detach())), grads, batch_input
 
 
 def gumbel_uniform(seed: int, n: int, step: int, k: np.ndarray) -> np.ndarray:

@@ -56,6 +56,59 @@ def main():
                "dtype": a.dtype, "data": "synthetic uniform codes, random-init weights",
                "config": {"workload": "BASELINE config 4 (per GPU)", "batch": a.batch, "ctx": a.ctx, "bins": a.bins,
                           **kw}, "loss": float(pr.results()["loss"])}
+        # kernel-level rooflines of the step's dominant pieces, timed as hipGraph replays (HIP events on the
+        # launching stream): the sequence-linear layer (HBM-bound: bytes = X + Y + residual), the row
+        # attention forward and the fused head (MFMA work, exp-heavy)
+        import vqa_lib as V
+        M = a.batch * a.ctx
+        cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+        esz = 2 if a.dtype == "bf16" else 4
+        x = torch.randn(a.batch, a.ctx, 128, device=dev).to(cdt)
+        r = torch.randn_like(x)
+        y = torch.empty_like(x)
+        w = torch.randn(128, 128, device=dev) * 0.05
+        bb = torch.zeros(128, device=dev)
+        q = torch.randn(a.batch, a.ctx, 32, device=dev).to(cdt)
+        o = torch.empty_like(q)
+        lse = torch.empty(a.batch, a.ctx, 2, device=dev)
+        wt = torch.empty(a.bins, 128, dtype=cdt, device=dev)
+        V.head_wt(torch.randn(128, a.bins, device=dev) * 0.05, wt)
+        hb = torch.zeros(a.bins, device=dev)
+        hl = torch.empty(M, device=dev)
+        am = torch.empty(M, dtype=torch.int64, device=dev)
+
+        def timed(fn, reps=20):
+            fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    fn()
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / reps * 1e3  # us
+
+        wp = torch.empty(1, 128, 128, dtype=cdt, device=dev)
+        V.seqlin_prep([(w, wp, 1, 128, 128, False)], cdt)
+        t_lin = timed(lambda: V.seqlin_fwd_prepped(x, wp, bb, y, a.ctx, residual=r))
+        lin_bytes = 3 * M * 128 * esz
+        t_att = timed(lambda: V.attn_fwd(q, q, q, o, lse, 0, a.ctx // 4, 2, 0.25))
+        att_flop = a.batch * 2 * 4 * (a.ctx // 4) * (a.ctx // 4 + 64) / 2 * 16 * 2 * 2
+        t_head = timed(lambda: V.head_fwd(x, wt, hb, hl, amax=am))
+        head_flop = 2.0 * M * 128 * a.bins
+        out["roofline"] = {"kernel": "seqlin_kernel<bf16> (Dense 128->128 + residual, the mlp / proj form)",
+                           "bound": "hbm", "achieved": round(lin_bytes / t_lin / 1e3, 1), "peak": 8000.0,
+                           "unit": "GB/s", "frac": round(lin_bytes / t_lin / 1e3 / 8000.0, 4),
+                           "avg_launch_us": round(t_lin, 2), "algorithmic_bytes_per_launch": lin_bytes}
+        out["kernels"] = {
+            "attn_fwd_row": {"us": round(t_att, 1), "tflops": round(att_flop / t_att / 1e6, 1),
+                             "mfma_frac": round(att_flop / t_att / 1e6 / 2500.0, 4)},
+            "head_fwd": {"us": round(t_head, 1), "tflops": round(head_flop / t_head / 1e6, 1),
+                         "mfma_frac": round(head_flop / t_head / 1e6 / 2500.0, 4)}}
         if not a.no_cpu:
             import numpy as np
             from oracle import prior_ref as P

@@ -16,6 +16,7 @@
 #include "vqa_mfma.h"
 #include <algorithm>
 #include <math.h>
+#include <type_traits>
 
 namespace vqa {
 
@@ -62,6 +63,7 @@ __device__ __forceinline__ float wave_max_f(float v) {
 struct SeqLinArgs {
   const void* x;
   const float* w;
+  const void* wp;  // optional: weights prepared by vqa_seqlin_prep as [taps][N][K] in the activation dtype
   const float* b;
   const void* r;
   void* y;
@@ -101,6 +103,15 @@ __global__ __launch_bounds__(256) void seqlin_kernel(SeqLinArgs a) {
   const int kof = M::koff(lane), col = lane & 15;
   for (int tap = 0; tap < a.taps; ++tap) {
     if (tap) __syncthreads();  // every read of the previous tap's weights is done
+    if (a.wp) {  // prepared image rows: straight 16-byte copies
+      constexpr int VEC = 16 / (int)sizeof(T);
+      const T* wp = (const T*)a.wp + (size_t)tap * a.K * a.N;
+      const int cpr = a.K / VEC;
+      for (int e = threadIdx.x; e < a.N * cpr; e += 256) {
+        const int n = e / cpr, q = e - n * cpr;
+        *(uint4*)(Wt + n * KS + q * VEC) = *(const uint4*)(wp + (size_t)n * a.K + q * VEC);
+      }
+    } else {
     const float* w = a.w + (size_t)tap * a.K * a.N;
     // 16-byte coalesced weight reads (4 consecutive elements of the contiguous axis)
     for (int e4 = threadIdx.x; e4 < a.K * a.N / 4; e4 += 256) {
@@ -113,6 +124,7 @@ __global__ __launch_bounds__(256) void seqlin_kernel(SeqLinArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) Wt[(n + i) * KS + k] = (T)v[i];
       }
+    }
     }
     __syncthreads();
     // row j of X for output row i: i + dir * (taps - 1 - tap) + lo
@@ -148,6 +160,136 @@ __global__ __launch_bounds__(256) void seqlin_kernel(SeqLinArgs a) {
       if (a.accumulate) v = v + ld4((const T*)yp);
       st4(yp, v);
     }
+  }
+}
+
+// 4 consecutive activation elements kept raw (bf16: 8 bytes, fp32: 16 bytes) and widened when used
+template <class T> struct RawR4;
+template <> struct RawR4<bf16> {
+  typedef uint2 type;
+  type v;
+  __device__ __forceinline__ f32x4 f() const {
+    const bf16x4 b = __builtin_bit_cast(bf16x4, v);
+    return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+  }
+};
+template <> struct RawR4<float> {
+  typedef uint4 type;
+  type v;
+  __device__ __forceinline__ f32x4 f() const { return __builtin_bit_cast(f32x4, v); }
+};
+
+// Persistent direct form for prepared weights (the prior's shapes, K and taps compile-time): the weight images
+// of every tap staged ONCE per workgroup in LDS; each wave takes 16 rows of a 64-row tile and loads its B
+// fragments (X^T: lane (row, g) <- 8 consecutive channels of its row) straight from global memory into
+// registers — no LDS copy of X, no barrier per tile — with the NEXT tile's fragments and residual rows
+// loaded while the current tile's MFMAs and stores run.
+constexpr int kSdRows = 64;
+
+template <class T, int K, int TAPS, int NT>
+__global__ __launch_bounds__(256) void seqlin_d_kernel(SeqLinArgs a, int ntiles) {
+  typedef Mfma<T> M;
+  typedef typename M::frag F;
+  constexpr int PAD = 16 / (int)sizeof(T), VEC = 16 / (int)sizeof(T), KS = K + PAD, NKC = K / M::KS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Wt = (T*)smem;  // [TAPS * N][K + PAD]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, kof = M::koff(lane),
+            g4 = 4 * (lane >> 4);
+  constexpr int CPR = K / VEC;
+  for (int e = threadIdx.x; e < TAPS * a.N * CPR; e += 256) {
+    const int n = e / CPR, q = e % CPR;
+    *(uint4*)(Wt + n * KS + q * VEC) = *(const uint4*)((const T*)a.wp + (size_t)n * K + q * VEC);
+  }
+  F bf[2][TAPS][NKC];
+  RawR4<T> rr[2][NT];  // residual chunks (4 channels) of the lane's row per output tile
+  // register double buffer: the slot is a compile-time constant (runtime-indexed register arrays spill)
+  auto load_tile = [&](int tile, auto S) {
+    constexpr int slot = decltype(S)::value;
+    const int seq = tile / a.tiles_per_seq, t = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16 + col;
+#pragma unroll
+    for (int tap = 0; tap < TAPS; ++tap) {
+      const int src = t + a.dir * (TAPS - 1 - tap);
+      const bool ok = src >= 0 && src < a.T && t < a.T;
+      const T* p = (const T*)a.x + ((long long)seq * a.T + (ok ? src : 0)) * a.ldx + kof;
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) {
+        F v = M::load(p + kc * M::KS);
+        if (!ok) v = F{};
+        bf[slot][tap][kc] = v;
+      }
+    }
+    if (a.r) {
+      const bool ok = t < a.T;
+      const T* rp = (const T*)a.r + ((long long)seq * a.T + (ok ? t : 0)) * a.ldr + g4;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        if (nt * 16 < a.N) rr[slot][nt].v = *(const typename RawR4<T>::type*)(rp + nt * 16);
+    }
+  };
+  auto compute = [&](int tile, auto S) {
+    constexpr int slot = decltype(S)::value;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < TAPS; ++tap)
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) {
+        const F b = bf[slot][tap][kc];
+        const T* wb = Wt + (tap * a.N + col) * KS + kof + kc * M::KS;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          if (nt * 16 >= a.N) break;
+          acc[nt] = M::mma(M::load(wb + nt * 16 * KS), b, acc[nt]);
+        }
+      }
+    const int seq = tile / a.tiles_per_seq, t = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16 + col;
+    if (t < a.T) {
+      const long long row = (long long)seq * a.T + t;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if (nt * 16 >= a.N) break;
+        const int c = nt * 16 + g4;
+        f32x4 v = acc[nt];
+        if (a.b) v = v + f32x4{a.b[c], a.b[c + 1], a.b[c + 2], a.b[c + 3]};
+        if (a.r) v = v + rr[slot][nt].f();
+        T* yp = (T*)a.y + row * a.ldy + c;
+        if (a.accumulate) v = v + ld4((const T*)yp);
+        st4(yp, v);
+      }
+    }
+  };
+  typedef std::integral_constant<int, 0> S0;
+  typedef std::integral_constant<int, 1> S1;
+  const int G = gridDim.x;
+  int tile = blockIdx.x;
+  if (tile < ntiles) load_tile(tile, S0());
+  __syncthreads();  // weight images staged
+  for (; tile < ntiles; tile += 2 * G) {
+    if (tile + G < ntiles) load_tile(tile + G, S1());
+    compute(tile, S0());
+    if (tile + G >= ntiles) break;
+    if (tile + 2 * G < ntiles) load_tile(tile + 2 * G, S0());
+    compute(tile + G, S1());
+  }
+}
+
+// Weight preparation for seqlin: out[tap][n][k] = Wv[tap][k][n] in the activation dtype, for a batch of layers in
+// one launch (blockIdx.y = descriptor). Run once per step; the forward passes and the data gradients then stage
+// their weights with plain 16-byte copies.
+constexpr int kMaxPrep = 48;
+struct PrepBatch {
+  vqa_seqlin_prep_desc d[kMaxPrep];
+};
+
+template <class T>
+__global__ __launch_bounds__(256) void seqlin_prep_kernel(PrepBatch b) {
+  const vqa_seqlin_prep_desc& d = b.d[blockIdx.y];
+  const int total = d.taps * d.K * d.N;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int tap = e / (d.N * d.K), rem = e - tap * d.N * d.K, n = rem / d.K, k = rem - n * d.K;
+    const float v = d.wtrans ? d.w[((size_t)tap * d.N + n) * d.K + k] : d.w[((size_t)tap * d.K + k) * d.N + n];
+    ((T*)d.out)[e] = (T)v;
   }
 }
 
@@ -1326,6 +1468,30 @@ static int set_lds_attr(const void* fn, size_t bytes) {
 
 template <class T>
 static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
+  if (a.wp) {
+    const int KS = a.K + 16 / (int)sizeof(T);
+    const size_t lds = (size_t)a.taps * a.N * KS * sizeof(T);
+    const void* fn = nullptr;
+    const bool n2 = a.N <= 32;
+#define VQA_SD(KK, TT)                                                                                  \
+    if (a.K == KK && a.taps == TT)                                                                    \
+      fn = n2 ? (const void*)seqlin_d_kernel<T, KK, TT, 2> : (const void*)seqlin_d_kernel<T, KK, TT, 8>;
+    VQA_SD(32, 1) VQA_SD(128, 1) VQA_SD(96, 3) VQA_SD(128, 3)
+#undef VQA_SD
+    if (fn && lds <= 160 * 1024) {
+      if (int rc = set_lds_attr(fn, lds)) return rc;
+      SeqLinArgs c = a;
+      c.tiles_per_seq = (a.T + kSdRows - 1) / kSdRows;
+      int ntiles = a.nseq * c.tiles_per_seq;
+      const int per_cu = std::max(1, std::min<int>(2, (int)(160 * 1024 / lds)));
+      const int nwg = std::min(ntiles, pr_cus() * per_cu);
+      void* args[] = {&c, &ntiles};
+      (void)hipLaunchKernel(fn, dim3(nwg), dim3(256), args, lds, s);
+      VQA_LAUNCHED("seqlin_d_kernel");
+      return VQA_OK;
+    }
+    // weights too large for one LDS image: stage per tap from the prepared image
+  }
   const void* fn = a.N <= 32 ? (const void*)seqlin_kernel<T, 2> : (const void*)seqlin_kernel<T, 8>;
   const size_t lds = seqlin_lds(a.K, a.N, a.taps, sizeof(T));
   if (int rc = set_lds_attr(fn, lds)) return rc;
@@ -1355,10 +1521,29 @@ static void wgrad_plan(int nseq, int T, int& seg_rows, int& segs) {
 
 using namespace vqa;
 
-extern "C" int vqa_seqlin_fwd(const void* x, int64_t ldx, const float* w, const float* bias, const void* residual,
-                              int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K, int N, int taps, int dir,
-                              int wtrans, int accumulate, int dtype, vqa_stream_t stream) {
-  VQA_ARG(x && w && y && nseq > 0 && T > 0 && (taps == 1 || taps == 3) && (dir == -1 || dir == 1),
+extern "C" int vqa_seqlin_prep(const vqa_seqlin_prep_desc* descs, int count, int dtype, vqa_stream_t stream) {
+  VQA_ARG(descs && count > 0 && pr_dt(dtype), "seqlin_prep: bad arguments");
+  for (int i0 = 0; i0 < count; i0 += kMaxPrep) {
+    PrepBatch b;
+    const int n = std::min(kMaxPrep, count - i0);
+    for (int i = 0; i < n; ++i) {
+      b.d[i] = descs[i0 + i];
+      VQA_ARG(b.d[i].w && b.d[i].out && b.d[i].taps > 0 && b.d[i].K > 0 && b.d[i].N > 0, "seqlin_prep: descriptor %d",
+              i0 + i);
+    }
+    if (dtype == VQA_BF16)
+      hipLaunchKernelGGL(seqlin_prep_kernel<bf16>, dim3(16, n), dim3(256), 0, (hipStream_t)stream, b);
+    else
+      hipLaunchKernelGGL(seqlin_prep_kernel<float>, dim3(16, n), dim3(256), 0, (hipStream_t)stream, b);
+    VQA_LAUNCHED("seqlin_prep_kernel");
+  }
+  return VQA_OK;
+}
+
+static int seqlin_launch(const void* x, int64_t ldx, const float* w, const void* wp, const float* bias,
+                         const void* residual, int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K, int N,
+                         int taps, int dir, int wtrans, int accumulate, int dtype, hipStream_t s) {
+  VQA_ARG(x && (w || wp) && y && nseq > 0 && T > 0 && (taps == 1 || taps == 3) && (dir == -1 || dir == 1),
           "seqlin_fwd: bad arguments");
   VQA_ARG(pr_dt(dtype), "seqlin_fwd: unknown dtype %d", dtype);
   const int esz = dtype == VQA_BF16 ? 2 : 4, vec = 16 / esz;
@@ -1366,11 +1551,26 @@ extern "C" int vqa_seqlin_fwd(const void* x, int64_t ldx, const float* w, const 
               VQA_E_UNSUPPORTED, "seqlin_fwd: K=%d N=%d unsupported", K, N);
   VQA_ARG(ldx % vec == 0 && ldy % 4 == 0 && (!residual || ldr % 4 == 0) && ldx >= K && ldy >= N,
           "seqlin_fwd: strides must keep 16-byte rows");
-  VQA_ARG(((uintptr_t)w & 15) == 0, "seqlin_fwd: weights must be 16-byte aligned");
-  SeqLinArgs a{x, w, bias, residual, y, ldx, ldr, ldy, nseq, T, K, N, taps, dir, wtrans, accumulate,
+  VQA_ARG(((uintptr_t)(w ? (const void*)w : wp) & 15) == 0, "seqlin_fwd: weights must be 16-byte aligned");
+  SeqLinArgs a{x, w, wp, bias, residual, y, ldx, ldr, ldy, nseq, T, K, N, taps, dir, wtrans, accumulate,
                (T + kSlRows - 1) / kSlRows};
-  hipStream_t s = (hipStream_t)stream;
   return dtype == VQA_BF16 ? launch_seqlin<bf16>(a, s) : launch_seqlin<float>(a, s);
+}
+
+extern "C" int vqa_seqlin_fwd(const void* x, int64_t ldx, const float* w, const float* bias, const void* residual,
+                              int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K, int N, int taps, int dir,
+                              int wtrans, int accumulate, int dtype, vqa_stream_t stream) {
+  VQA_ARG(w, "seqlin_fwd: no weights");
+  return seqlin_launch(x, ldx, w, nullptr, bias, residual, ldr, y, ldy, nseq, T, K, N, taps, dir, wtrans, accumulate,
+                       dtype, (hipStream_t)stream);
+}
+
+extern "C" int vqa_seqlin_fwd_prepped(const void* x, int64_t ldx, const void* wp, const float* bias,
+                                      const void* residual, int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K,
+                                      int N, int taps, int dir, int accumulate, int dtype, vqa_stream_t stream) {
+  VQA_ARG(wp, "seqlin_fwd_prepped: no weights");
+  return seqlin_launch(x, ldx, nullptr, wp, bias, residual, ldr, y, ldy, nseq, T, K, N, taps, dir, 0, accumulate,
+                       dtype, (hipStream_t)stream);
 }
 
 extern "C" size_t vqa_seqlin_wgrad_workspace(int nseq, int T, int K, int N, int taps) {

@@ -107,6 +107,28 @@ class ResidualAttnBlock:
         store.add(f"{prefix}/mlp/kernel", (d, self.mlp_width), "glorot_uniform")
         store.add(f"{prefix}/mlp/bias", (self.mlp_width,), "zeros")
 
+    # -------------------------------------------------------------- weight images (vqa_seqlin_prep)
+    def prep_descs(self, cdt, device, bwd):
+        """(w, out, taps, K, N, wtrans) of every linear map: forward images, and with bwd the transposed images
+        of the data gradients. The buffers persist; their contents are refreshed once per step."""
+        f, st, pre, d, w = self.fmha, self.store, self.prefix, self.d_model, self.fmha.width
+        maps = {"qkv": (f"{pre}/qkv/kernel", 3, d, 3 * w), "query": (f"{pre}/mha/query/kernel", 1, w, w),
+                "key": (f"{pre}/mha/key/kernel", 1, w, w), "value": (f"{pre}/mha/value/kernel", 1, w, w),
+                "out": (f"{pre}/mha/out/kernel", 1, w, w), "proj": (f"{pre}/proj/kernel", 1, w, d),
+                "mlp": (f"{pre}/mlp/kernel", 1, d, self.mlp_width)}
+        if not hasattr(self, "wp") or self._wp_dtype != cdt:
+            self.wp, self._wp_dtype = {}, cdt
+        out = []
+        for name, (pname, taps, K, N) in maps.items():
+            for tr in ((False, True) if bwd else (False,)):
+                key = name + ("_T" if tr else "")
+                Ki, Ni = (N, K) if tr else (K, N)
+                if key not in self.wp:
+                    self.wp[key] = torch.empty(taps, Ni, Ki, dtype=cdt, device=device)
+                # forward: Wv = W (K, N); transposed (data gradient): Wv[k=out][n=in] = W[n][k] -> wtrans
+                out.append((st.view(pname), self.wp[key], taps, Ki, Ni, tr))
+        return out
+
     # -------------------------------------------------------------- forward / backward on the device
     def forward(self, x, T, training, save, seed, salt, counter=None):
         """x (N, T, d) -> (N, T, d). save: keep what backward needs (layer input, qkv, heads, lse, o32, x1)."""
@@ -117,11 +139,12 @@ class ResidualAttnBlock:
                         eps)
         w = f.width
         qkv = torch.empty(N, T, 3 * w, dtype=cdt, device=x.device)
-        V.seqlin_fwd(a, f.p("qkv/kernel"), f.p("qkv/bias"), qkv, T, taps=3, dir=-1)
+        wp = self.wp
+        V.seqlin_fwd_prepped(a, wp["qkv"], f.p("qkv/bias"), qkv, T, taps=3, dir=-1)
         heads = []
         for j, n in enumerate(("query", "key", "value")):
             h = torch.empty(N, T, w, dtype=cdt, device=x.device)
-            V.seqlin_fwd(qkv[..., j * w:(j + 1) * w], f.p(f"mha/{n}/kernel"), f.p(f"mha/{n}/bias"), h, T)
+            V.seqlin_fwd_prepped(qkv[..., j * w:(j + 1) * w], wp[n], f.p(f"mha/{n}/bias"), h, T)
             heads.append(h)
         qh, kh, vh = heads
         oh = torch.empty_like(qh)
@@ -129,21 +152,20 @@ class ResidualAttnBlock:
         V.attn_fwd(qh, kh, vh, oh, lse, f.attn_func, f.block_len, f.num_heads, 1.0 / math.sqrt(f.head_dim),
                    vbias=f.p("mha/value/bias"))
         o32 = torch.empty_like(qh)
-        V.seqlin_fwd(oh, f.p("mha/out/kernel"), f.p("mha/out/bias"), o32, T)
+        V.seqlin_fwd_prepped(oh, wp["out"], f.p("mha/out/bias"), o32, T)
         x1 = torch.empty_like(x)
         drop = training and f.rate > 0
         if drop:
-            V.seqlin_fwd(o32, f.p("proj/kernel"), f.p("proj/bias"), x1, T)
+            V.seqlin_fwd_prepped(o32, wp["proj"], f.p("proj/bias"), x1, T)
             V.dropout_(x1, f.rate, seed, salt, counter)
             V.axpy(x1, x, x1)
         else:
-            V.seqlin_fwd(o32, f.p("proj/kernel"), f.p("proj/bias"), x1, T, residual=x)
+            V.seqlin_fwd_prepped(o32, wp["proj"], f.p("proj/bias"), x1, T, residual=x)
         h2 = torch.empty_like(x)
         V.layernorm_fwd(x1, self.store.view(f"{self.prefix}/ln2/gamma"), self.store.view(f"{self.prefix}/ln2/beta"),
                         h2, eps)
         out = torch.empty_like(x)
-        V.seqlin_fwd(h2, self.store.view(f"{self.prefix}/mlp/kernel"), self.store.view(f"{self.prefix}/mlp/bias"),
-                     out, T, residual=x1)
+        V.seqlin_fwd_prepped(h2, wp["mlp"], self.store.view(f"{self.prefix}/mlp/bias"), out, T, residual=x1)
         self._saved = (x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter) if save else None
         return out
 
@@ -157,7 +179,8 @@ class ResidualAttnBlock:
         h2 = torch.empty_like(x)
         V.layernorm_fwd(x1, st.view(f"{pre}/ln2/gamma"), st.view(f"{pre}/ln2/beta"), h2, eps)
         dh2 = torch.empty_like(x)
-        V.seqlin_fwd(dout, st.view(f"{pre}/mlp/kernel"), None, dh2, T, wtrans=True)
+        wp = self.wp
+        V.seqlin_fwd_prepped(dout, wp["mlp_T"], None, dh2, T)
         V.seqlin_wgrad(h2, dout, st.grad_view(f"{pre}/mlp/kernel"), st.grad_view(f"{pre}/mlp/bias"), T,
                        deferred=deferred)
         dx1 = torch.empty_like(x)
@@ -170,10 +193,10 @@ class ResidualAttnBlock:
             dres1 = dx1.clone()
             V.dropout_(dres1, f.rate, seed, salt, counter)
         do32 = torch.empty_like(qh)
-        V.seqlin_fwd(dres1, f.p("proj/kernel"), None, do32, T, wtrans=True)
+        V.seqlin_fwd_prepped(dres1, wp["proj_T"], None, do32, T)
         V.seqlin_wgrad(o32, dres1, f.g("proj/kernel"), f.g("proj/bias"), T, deferred=deferred)
         doh = torch.empty_like(qh)
-        V.seqlin_fwd(do32, f.p("mha/out/kernel"), None, doh, T, wtrans=True)
+        V.seqlin_fwd_prepped(do32, wp["out_T"], None, doh, T)
         V.seqlin_wgrad(oh, do32, f.g("mha/out/kernel"), f.g("mha/out/bias"), T, deferred=deferred)
         dqh, dkh, dvh = torch.empty_like(qh), torch.empty_like(qh), torch.empty_like(qh)
         dsum = torch.empty(N, T, f.num_heads, dtype=torch.float32, device=x.device)
@@ -189,13 +212,13 @@ class ResidualAttnBlock:
             post_adds.append((f.g("mha/value/bias").view(-1), extra))
         dqkv = torch.empty_like(qkv)
         for j, (n, dh) in enumerate((("query", dqh), ("key", dkh), ("value", dvh))):
-            V.seqlin_fwd(dh, f.p(f"mha/{n}/kernel"), None, dqkv[..., j * w:(j + 1) * w], T, wtrans=True)
+            V.seqlin_fwd_prepped(dh, wp[f"{n}_T"], None, dqkv[..., j * w:(j + 1) * w], T)
             V.seqlin_wgrad(qkv[..., j * w:(j + 1) * w], dh, f.g(f"mha/{n}/kernel"), f.g(f"mha/{n}/bias"), T,
                            deferred=deferred)
         a = torch.empty_like(x)
         V.layernorm_fwd(x, st.view(f"{pre}/ln1/gamma"), st.view(f"{pre}/ln1/beta"), a, eps)
         da = torch.empty_like(x)
-        V.seqlin_fwd(dqkv, f.p("qkv/kernel"), None, da, T, taps=3, dir=1, wtrans=True)
+        V.seqlin_fwd_prepped(dqkv, wp["qkv_T"], None, da, T, taps=3, dir=1)
         V.seqlin_wgrad(a, dqkv, f.g("qkv/kernel"), f.g("qkv/bias"), T, taps=3, deferred=deferred)
         dx = torch.empty_like(x)
         V.layernorm_bwd(x, da, st.view(f"{pre}/ln1/gamma"), dx, st.grad_view(f"{pre}/ln1/gamma"),
@@ -302,8 +325,19 @@ class FMHABasedAutoregressiveModel:
                           ycond=y_cond, xcond=x_cond, rate=self.rate if training else 0.0, seed=seed, counter=counter)
         return x
 
-    def hidden(self, tokens, training=False, x_cond=None, y_cond=None, save=False, seed=0, counter=None):
+    def prep_weights(self, bwd=False):
+        """Refresh every layer's weight images in one launch (vqa_seqlin_prep): forward, and with bwd the
+        transposed images of the data gradients."""
+        descs = []
+        for ly in self.transformer.layers:
+            descs += ly.prep_descs(self.cdt, self.device, bwd)
+        V.seqlin_prep(descs, self.cdt)
+
+    def hidden(self, tokens, training=False, x_cond=None, y_cond=None, save=False, seed=0, counter=None,
+               prepped=False):
         """Embedding + transformer: (N, T) tokens -> (N, T, d) final hidden state (the head's input)."""
+        if not prepped:
+            self.prep_weights(bwd=False)
         tokens = tokens.contiguous()
         T = tokens.shape[1]
         if self.use_pos_embedding and T > self.context_length:
@@ -472,13 +506,14 @@ class Prior:
         ctr = self.optimizer.iterations
         row_offset = vqa_dp.rank(self.process_group) * M
         xc = m._cond(upper, save=True) if upper is not None else None
+        m.prep_weights(bwd=True)
         # pass 1: teacher-forced input, argmax of the logits (prior.py:277-282)
         latent = torch.empty_like(codes)
         V.tf_mix(codes, None, None, latent, m.start_token)
         wt = m._wt(m.cdt)
         b = st.view(m.out_bias)
         with torch.no_grad():
-            h0 = m.hidden(latent, True, xc, seed=seed * 7919 + 1, counter=ctr)
+            h0 = m.hidden(latent, True, xc, seed=seed * 7919 + 1, counter=ctr, prepped=True)
             lse0 = torch.empty(M, dtype=torch.float32, device=dev)
             amax = torch.empty(N, T, dtype=torch.int64, device=dev)
             V.head_fwd(h0, wt, b, lse0, amax=amax)
@@ -488,7 +523,7 @@ class Prior:
         mask = None if tf_mask is None else torch.as_tensor(tf_mask, device=dev).to(torch.uint8).contiguous()
         V.tf_mix(codes, amax, mask, batch_input, m.start_token, rate=float(teacher_force_rate), seed=seed,
                  counter=ctr, row_offset=row_offset)
-        h = m.hidden(batch_input, True, xc, save=True, seed=seed * 7919 + 2, counter=ctr)
+        h = m.hidden(batch_input, True, xc, save=True, seed=seed * 7919 + 2, counter=ctr, prepped=True)
         lse = torch.empty(M, dtype=torch.float32, device=dev)
         loss_row = torch.empty(M, dtype=torch.float32, device=dev)
         correct = torch.empty(M, dtype=torch.float32, device=dev)

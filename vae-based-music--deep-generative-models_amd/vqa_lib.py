@@ -36,7 +36,7 @@ EXPORTED = [
     "vqa_step_metrics", "vqa_synthetic_batch",
     "vqa_embedding_fwd", "vqa_embedding_bwd", "vqa_embedding_bwd_workspace", "vqa_layernorm_fwd",
     "vqa_layernorm_bwd", "vqa_layernorm_bwd_workspace",
-    "vqa_seqlin_fwd", "vqa_seqlin_wgrad_workspace", "vqa_seqlin_wgrad", "vqa_prior_embed_fwd", "vqa_colsum",
+    "vqa_seqlin_fwd", "vqa_seqlin_prep", "vqa_seqlin_fwd_prepped", "vqa_seqlin_wgrad_workspace", "vqa_seqlin_wgrad", "vqa_prior_embed_fwd", "vqa_colsum",
     "vqa_axpy", "vqa_dropout", "vqa_scale_f32", "vqa_tf_mix", "vqa_attn_fwd", "vqa_attn_bwd", "vqa_head_wt",
     "vqa_head_fwd", "vqa_head_bwd_workspace", "vqa_head_bwd", "vqa_rowsum_workspace", "vqa_rowsum", "vqa_prior_decode_cache_bytes",
     "vqa_prior_decode",
@@ -115,6 +115,8 @@ _SIGS = {
     "vqa_spectral_loss_target": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _S, _P]),
     # factorized-attention prior
     "vqa_seqlin_fwd": (_I, [_P, _L, _P, _P, _P, _L, _P, _L] + [_I] * 9 + [_P]),
+    "vqa_seqlin_prep": (_I, [_P, _I, _I, _P]),
+    "vqa_seqlin_fwd_prepped": (_I, [_P, _L, _P, _P, _P, _L, _P, _L] + [_I] * 8 + [_P]),
     "vqa_seqlin_wgrad_workspace": (_S, [_I] * 5),
     "vqa_seqlin_wgrad": (_I, [_P, _L, _P, _L, _P, _P] + [_I] * 6 + [_P, _S, _P, _P]),
     "vqa_prior_embed_fwd": (_I, [_P] * 6 + [_I] * 4 + [_F, _F, _U, _P, _I, _P]),
@@ -553,6 +555,31 @@ def seqlin_fwd(x, w, b, y, T, taps=1, dir=-1, wtrans=False, residual=None, accum
     _check(lib().vqa_seqlin_fwd(px, ldx, ptr(w), ptr(b), pr, ldr, py, ldy, rows // T, T, K, N, taps, dir,
                                 int(bool(wtrans)), int(bool(accumulate)), dtype_code(x.dtype), stream()),
            "vqa_seqlin_fwd")
+
+
+class SeqlinPrepDesc(ctypes.Structure):
+    """vqa_seqlin_prep_desc (include/vqa.h)."""
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p), ("taps", ctypes.c_int), ("K", ctypes.c_int),
+                ("N", ctypes.c_int), ("wtrans", ctypes.c_int)]
+
+
+def seqlin_prep(descs, dtype):
+    """One launch converting a list of (w fp32 tensor, out tensor, taps, K, N, wtrans) to [taps][N][K] images."""
+    arr = (SeqlinPrepDesc * len(descs))(*[SeqlinPrepDesc(ptr(w).value, ptr(o).value, t, k, n, int(bool(tr)))
+                                         for (w, o, t, k, n, tr) in descs])
+    _check(lib().vqa_seqlin_prep(arr, len(descs), dtype_code(dtype), stream()), "vqa_seqlin_prep")
+
+
+def seqlin_fwd_prepped(x, wp, b, y, T, taps=1, dir=-1, residual=None, accumulate=False):
+    """vqa_seqlin_fwd_prepped: wp = (taps, N, K) image in the activation dtype (seqlin_prep)."""
+    px, ldx = rptr(x)
+    py, ldy = rptr(y)
+    pr, ldr = rptr(residual) if residual is not None else (None, 0)
+    K, N = x.shape[-1], y.shape[-1]
+    rows = x.numel() // K
+    _check(lib().vqa_seqlin_fwd_prepped(px, ldx, ptr(wp), ptr(b), pr, ldr, py, ldy, rows // T, T, K, N, taps, dir,
+                                        int(bool(accumulate)), dtype_code(x.dtype), stream()),
+           "vqa_seqlin_fwd_prepped")
 
 
 def seqlin_wgrad(x, dy, dw, db, T, taps=1, deferred=None):
