@@ -564,6 +564,9 @@ struct AttnArgs {
   float scale;
 };
 
+// raw v_exp_f32 (no denormal range handling: probabilities below 2^-126 flush to zero, as in any softmax)
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ float grp_max(float v) {
   v = fmaxf(v, __shfl_xor(v, 16, 64));
   return fmaxf(v, __shfl_xor(v, 32, 64));
@@ -583,6 +586,21 @@ __device__ __forceinline__ void stage64(T* dst, const T* src, long long row0, in
   if constexpr (sizeof(T) == 2) *(uint2*)(dst + r * AKS + q) = *(const uint2*)p;
   else *(uint4*)(dst + r * AKS + q) = *(const uint4*)p;
 }
+
+// the calling thread's 4-element chunk of a 64 x 16 tile, held in registers between the global load (issued one
+// tile ahead) and the LDS store
+template <class T> struct Chunk64 {
+  typedef typename std::conditional<sizeof(T) == 2, uint2, uint4>::type V;
+  V v;
+  __device__ __forceinline__ void load(const T* src, long long row0, int H, int h) {
+    const int r = threadIdx.x >> 2, q = (threadIdx.x & 3) * 4;
+    v = *(const V*)(src + ((row0 + r) * H + h) * AHD + q);
+  }
+  __device__ __forceinline__ void store(T* dst) const {
+    const int r = threadIdx.x >> 2, q = (threadIdx.x & 3) * 4;
+    *(V*)(dst + r * AKS + q) = v;
+  }
+};
 
 template <class T, int MODE>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
@@ -605,32 +623,47 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const float c = a.scale * kLog2e;
   float m = -INFINITY, lsum = 0.f;
   f32x4 oacc = {0.f, 0.f, 0.f, 0.f};
+  Chunk64<T> ck, cv;
+  ck.load((const T*)a.k, (long long)n * a.T + kt0 * 64, a.H, h);
+  cv.load((const T*)a.v, (long long)n * a.T + kt0 * 64, a.H, h);
   for (int kt = kt0; kt <= kt1; ++kt) {
     __syncthreads();
-    stage64<T>(Ks, (const T*)a.k, (long long)n * a.T + kt * 64, a.H, h);
-    stage64<T>(Vs, (const T*)a.v, (long long)n * a.T + kt * 64, a.H, h);
+    ck.store(Ks);
+    cv.store(Vs);
     __syncthreads();
+    if (kt < kt1) {  // next tile in flight while this one computes
+      ck.load((const T*)a.k, (long long)n * a.T + (kt + 1) * 64, a.H, h);
+      cv.load((const T*)a.v, (long long)n * a.T + (kt + 1) * 64, a.H, h);
+    }
+    // raw scores; the scale (> 0) is applied inside the exponent: p = 2^(s*c - m), m = max(s)*c
     float x[4][4];
     float mt = -INFINITY;
+    const bool diag = MODE == 0 && kt == qt;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const f32x4 s = A::mm_d(A::ld_d(Ks + (st * 16 + li) * AKS), qf, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x[st][i] = s[i] * c;
-        if (MODE == 0 && kt == qt && st * 16 + 4 * g + i > wave * 16 + li) x[st][i] = -INFINITY;
-        mt = fmaxf(mt, x[st][i]);
-      }
+      for (int i = 0; i < 4; ++i) x[st][i] = s[i];
     }
-    mt = grp_max(mt);
-    const float mn = fmaxf(m, mt), alpha = exp2f(m - mn);
+    if (diag) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (st * 16 + 4 * g + i > wave * 16 + li) x[st][i] = -INFINITY;
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      mt = fmaxf(fmaxf(fmaxf(mt, x[st][0]), fmaxf(x[st][1], x[st][2])), x[st][3]);
+    mt = grp_max(mt) * c;
+    const float mn = fmaxf(m, mt), alpha = fexp2(m - mn);
     m = mn;
     float p[4][4], ps = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        p[st][i] = exp2f(x[st][i] - mn);
+        p[st][i] = fexp2(__builtin_fmaf(x[st][i], c, -mn));
         ps += p[st][i];
       }
     lsum = lsum * alpha + ps;
@@ -670,11 +703,18 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
   const int kt0 = MODE == 0 ? b * a.l / 64 : (b - 1) * a.l / 64, kt1 = MODE == 0 ? qt : b * a.l / 64 - 1;
   const float c = a.scale * kLog2e;
   f32x4 dqacc = {0.f, 0.f, 0.f, 0.f};
+  Chunk64<T> ck, cv;
+  ck.load((const T*)a.k, (long long)n * a.T + kt0 * 64, a.H, h);
+  cv.load((const T*)a.v, (long long)n * a.T + kt0 * 64, a.H, h);
   for (int kt = kt0; kt <= kt1; ++kt) {
     __syncthreads();
-    stage64<T>(Ks, (const T*)a.k, (long long)n * a.T + kt * 64, a.H, h);
-    stage64<T>(Vs, (const T*)a.v, (long long)n * a.T + kt * 64, a.H, h);
+    ck.store(Ks);
+    cv.store(Vs);
     __syncthreads();
+    if (kt < kt1) {
+      ck.load((const T*)a.k, (long long)n * a.T + (kt + 1) * 64, a.H, h);
+      cv.load((const T*)a.v, (long long)n * a.T + (kt + 1) * 64, a.H, h);
+    }
     float ds[4][4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
@@ -682,7 +722,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
       const f32x4 dp = A::mm_d(A::ld_d(Vs + (st * 16 + li) * AKS), dof, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float p = exp2f(s[i] * c - lse);
+        float p = fexp2(__builtin_fmaf(s[i], c, -lse));
         if (MODE == 0 && kt == qt && st * 16 + 4 * g + i > wave * 16 + li) p = 0.f;
         ds[st][i] = p * (dp[i] - D);
       }
@@ -721,16 +761,28 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   const typename A::dfrag kf = A::ld_d((const T*)a.k + off), vf = A::ld_d((const T*)a.v + off);
   const float c = a.scale * kLog2e;
   f32x4 dkacc = {0.f, 0.f, 0.f, 0.f}, dvacc = {0.f, 0.f, 0.f, 0.f};
+  Chunk64<T> cq, cd;
+  float pl = 0.f, pd = 0.f;
+  auto load_q = [&](int qt) {
+    const long long r0 = (long long)n * a.T + qt * 64;
+    cq.load((const T*)a.q, r0, a.H, h);
+    cd.load((const T*)a.dout, r0, a.H, h);
+    if (threadIdx.x < 64) {
+      pl = a.lse[(r0 + threadIdx.x) * a.H + h];
+      pd = a.dsum[(r0 + threadIdx.x) * a.H + h];
+    }
+  };
+  if (qt0 <= qt1) load_q(qt0);
   for (int qt = qt0; qt <= qt1; ++qt) {
     __syncthreads();
-    const long long r0 = (long long)n * a.T + qt * 64;
-    stage64<T>(Qs, (const T*)a.q, r0, a.H, h);
-    stage64<T>(Ds, (const T*)a.dout, r0, a.H, h);
+    cq.store(Qs);
+    cd.store(Ds);
     if (threadIdx.x < 64) {
-      Ls[threadIdx.x] = a.lse[(r0 + threadIdx.x) * a.H + h];
-      Dd[threadIdx.x] = a.dsum[(r0 + threadIdx.x) * a.H + h];
+      Ls[threadIdx.x] = pl;
+      Dd[threadIdx.x] = pd;
     }
     __syncthreads();
+    if (qt < qt1) load_q(qt + 1);
     float p[4][4], ds[4][4];
 #pragma unroll
     for (int qs = 0; qs < 4; ++qs) {
@@ -739,7 +791,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ql = qs * 16 + 4 * g + i;
-        float pv = exp2f(s[i] * c - Ls[ql]);
+        float pv = fexp2(__builtin_fmaf(s[i], c, -Ls[ql]));
         if (MODE == 0 && qt == kt && wave * 16 + li > ql) pv = 0.f;
         p[qs][i] = pv;
         ds[qs][i] = pv * (dp[i] - Dd[ql]);
