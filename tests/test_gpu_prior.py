@@ -295,3 +295,93 @@ def test_prior_test_step_and_metrics(cuda):
     for t in pr.metrics:
         t.reset_state()
     assert float(pr.train_loss_tracker.result()) == 0.0
+
+
+# ------------------------------------------------------------------ dropout, conditioning
+def test_dropout_mask_statistics_and_determinism(cuda):
+    """keras Dropout(rate): kept elements scaled by 1/(1-rate), drop fraction = rate; counter-based mask:
+    the same (seed, salt, counter) gives the same mask, another counter a different one."""
+    import vqa_lib as V
+    rate = 0.1
+    x = torch.ones(1 << 20, device="cuda")
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    a = x.clone()
+    V.dropout_(a, rate, 7, 3, ctr)
+    b = x.clone()
+    V.dropout_(b, rate, 7, 3, ctr)
+    ctr += 1
+    c = x.clone()
+    V.dropout_(c, rate, 7, 3, ctr)
+    torch.cuda.synchronize()
+    frac = float((a == 0).float().mean())
+    assert abs(frac - rate) < 3e-3
+    assert torch.equal(a[a != 0], torch.full_like(a[a != 0], 1.0 / (1.0 - rate)))
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    # the embedding's dropout: same statistics on (table row * scale + pos)
+    tok = torch.zeros(4, 4096, dtype=torch.int64, device="cuda")
+    table = torch.ones(8, 128, device="cuda")
+    pos = torch.zeros(4096, 128, device="cuda")
+    out = torch.empty(4, 4096, 128, device="cuda")
+    V.prior_embed_fwd(table, pos, tok, out, 1.0, rate=rate, seed=5)
+    torch.cuda.synchronize()
+    assert abs(float((out == 0).float().mean()) - rate) < 3e-3
+
+
+def test_conditioned_logits_and_decode_match_oracle(cuda):
+    """x_cond (an up-sampled upper level, autoregressive_fmha.py:142-151) and y_cond (a label embedding that
+    replaces position 0, :120-129): the model's logits and the decode kernel's teacher-forced logits vs the
+    oracle."""
+    m, p = _model(CFG)
+    g = _gen(31)
+    tok = torch.randint(0, CFG.bins, (2, CFG.ctx), generator=g)
+    tok[:, 0] = CFG.bins - 1
+    xc = torch.randn(2, CFG.ctx, CFG.width, generator=g) * 0.5
+    yc = torch.randn(2, CFG.width, generator=g) * 0.05
+    logits, _ = m(tok, x_cond=xc.cuda(), y_cond=yc.cuda())
+    ref = P.model_forward(p, CFG, tok, y_cond=yc.double()[:, None, :], x_cond=xc.double())
+    assert _rel(logits, ref) < 2e-5
+    L = 100
+    _, dl = m.sample(2, max_length=L, x_cond=xc.cuda(), y_cond=yc.cuda(), forced=tok[:, :L + 1].cuda(),
+                     return_logits=True, seed=1)
+    torch.cuda.synchronize()
+    ref = P.model_forward(p, CFG, tok[:, :L], y_cond=yc.double()[:, None, :], x_cond=xc.double())
+    assert _rel(dl, ref) < 2e-5
+
+
+def test_upsampler_train_step_with_conditioner_matches_oracle(cuda):
+    """The upsampler prior (level 0 of 2, ConditionerNet on the level-1 codes, Sampler.py:25): one train step
+    vs the oracle (conditioner_ref + prior_ref, fp64 autograd through both)."""
+    from oracle import conditioner_ref as C
+    from prior import Prior
+    cfg = P.PriorConfig(bins=64, ctx=256, width=128, depth=3, heads=2, blocks=4, attn_stacks=1)
+    ck = dict(dilation_factor=3, dilation_cycle=4, residual_width=32, residual_depth=8)
+    pr = Prior(0, [(cfg.ctx,), (cfg.ctx // 4,)], cfg.bins, [3, 2], [2, 2], None,
+               dict(width=128, depth=3, heads=2, blocks=4, attn_stacks=1, drop_out_rate=0.0), ck, dtype="fp32",
+               device="cuda", seed=5)
+    vals = pr.prior.store.values()
+    g = _gen(8)
+    codes = torch.randint(0, cfg.bins - 1, (2, cfg.ctx), generator=g)
+    upper = torch.randint(0, cfg.bins - 1, (2, cfg.ctx // 4), generator=g)
+    mask = torch.rand(2, cfg.ctx, generator=g) < 0.2
+    pt = {k: torch.from_numpy(v).double().requires_grad_(True) for k, v in vals.items()}
+
+    def xcond():
+        return C.conditioner_forward(pt, upper, "prior/conditioner", 2, 2, 8, 3, dilation_cycle=4)
+
+    start = cfg.bins - 1
+    latent = P.shift_right(codes, start)
+    with torch.no_grad():
+        pred = P.shift_right(P.argmax_lowest(P.model_forward(pt, cfg, latent, x_cond=xcond())), start)
+    bi = torch.where(mask, pred, latent)
+    loss = P.ce_loss(codes, P.model_forward(pt, cfg, bi, x_cond=xcond()))
+    loss.backward()
+    res = pr.train_step((codes.cuda(), upper.cuda()), tf_mask=mask.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(pr._last_batch_input.cpu(), bi)
+    assert abs(float(res["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
+    got = pr.prior.store.grads()
+    gmax = max(float(t.grad.abs().max()) for t in pt.values() if t.grad is not None)
+    for k, t in pt.items():
+        ref = t.grad if t.grad is not None else torch.zeros_like(t)
+        err = float((torch.from_numpy(got[k]).double() - ref).abs().max()) / max(float(ref.abs().max()), 1e-4 * gmax)
+        assert err < 5e-4, (k, err)

@@ -479,10 +479,18 @@ class Prior:
         return zs[self.level + 1][:, start // r:end // r]
 
     def _codes(self, x):
-        if isinstance(x, tuple):
-            x = x[0]
+        """Raw audio (N, T, 1) -> the VQ-VAE's codes of this level (and of the level above for the upsampler
+        conditioning, prior.py:257-260); int64 codes are taken as they are, as (codes, upper_codes) when the prior
+        is conditioned on the level above."""
+        if isinstance(x, (tuple, list)):
+            first = torch.as_tensor(x[0], device=self.device)
+            if first.dtype == torch.int64 and len(x) > 1 and self.prior.conditioner is not None:
+                return first.contiguous(), torch.as_tensor(x[1], device=self.device).long().contiguous()
+            x = first
         x = torch.as_tensor(x, device=self.device)
         if x.dtype == torch.int64:
+            if self.prior.conditioner is not None:
+                raise ValueError("a conditioned prior needs (codes, upper_level_codes)")
             return x.contiguous(), None
         codes = self.vqvae.encode(x, start_level=self.level, end_level=self.levels)
         upper = codes[1] if self.level != self.levels - 1 else None
