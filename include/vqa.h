@@ -306,7 +306,10 @@ int vqa_seqlin_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, f
                      vqa_stream_t stream);
 /* autoregressive_fmha.py:119-151: out = table[tokens] (row 0 <- ycond when given) * scale + pos[t]; keras
  * Dropout(rate) with a counter-based mask (seed, and the device step counter when given, so a replayed graph
- * draws a new mask each step); + xcond (N, T, W) when given. */
+ * draws a new mask each step); + xcond (N, T, W) when given. The mask is vqa_dropout's over the flat
+ * (N, T, W) index with salt VQA_EMB_DROPOUT_SALT: the gradient of the dropout is vqa_dropout(dx, N*T*W, rate,
+ * seed, VQA_EMB_DROPOUT_SALT, counter). */
+#define VQA_EMB_DROPOUT_SALT 0x454d42ull
 int vqa_prior_embed_fwd(const float* table, const float* pos, const int64_t* tokens, const float* ycond,
                         const void* xcond, void* out, int N, int T, int W, int bins, float scale, float rate,
                         uint64_t seed, const int64_t* counter, int dtype, vqa_stream_t stream);

@@ -16,8 +16,9 @@ Follows:
   src/autoregressive/autoregressive_fmha.py:162-240  sample (Gumbel noise, argmax)         -> sample_full_recompute
   autoregressive.py:189-212                        loss_function / accuracy_function    -> ce_loss, accuracy
   prior.py:241-335                                 Prior.train_step (teacher forcing, Adam) -> train_step
-Dropout is the identity here (rate 0, or training=False): TF's dropout RNG cannot be replayed; the product's
-counter-based dropout is tested by its statistics.
+Dropout: TF's dropout RNG cannot be replayed, so the masks are explicit multipliers (0 or 1/(1-rate)) passed in
+(`drop`); the GPU tests read the product's counter-based masks back and hand them over, and test the masks'
+statistics separately. Without masks dropout is the identity (rate 0, or training=False).
 Parity unpinned: TensorFlow is not importable and the reference holds no fixtures for the prior. The oracle is
 pinned by the reference's own sampling-consistency check (factorized_attention.py:446-462: every prefix call
 equals the full call at those positions, to 1e-6) and by hand-derived known answers (tests/test_oracle_prior.py).
@@ -195,35 +196,43 @@ def prev_row_attn(p, pre, q, k, v, l):
 ATTN = {0: row_attn, 1: col_attn, 2: prev_row_attn}
 
 
-def res_attn_block(p, pre, x, attn_type, l):
-    """transformer.py:35-60 with FactorizedAttention.call (factorized_attention.py:53-72)."""
+def res_attn_block(p, pre, x, attn_type, l, drop=None):
+    """transformer.py:35-60 with FactorizedAttention.call (factorized_attention.py:53-72). drop: the attention
+    output's keras Dropout as an explicit multiplier (0 or 1/(1-rate)), factorized_attention.py:51,72."""
     a = layer_norm(x, p[f"{pre}/ln1/gamma"], p[f"{pre}/ln1/beta"])
     qkv = causal_conv(a, p[f"{pre}/qkv/kernel"], p[f"{pre}/qkv/bias"])
     q, k, v = qkv.chunk(3, dim=-1)
     o = ATTN[attn_type](p, f"{pre}/mha", q, k, v, l)
     res1 = o @ p[f"{pre}/proj/kernel"] + p[f"{pre}/proj/bias"]
+    if drop is not None:
+        res1 = res1 * drop
     h = layer_norm(x + res1, p[f"{pre}/ln2/gamma"], p[f"{pre}/ln2/beta"])
     res2 = h @ p[f"{pre}/mlp/kernel"] + p[f"{pre}/mlp/bias"]
     return res2 + res1 + x
 
 
-def embed(p, cfg: PriorConfig, tokens, prefix="prior", y_cond=None, x_cond=None):
-    """autoregressive_fmha.py:119-151 (pos_emb=True; dropout = identity)."""
+def embed(p, cfg: PriorConfig, tokens, prefix="prior", y_cond=None, x_cond=None, drop=None):
+    """autoregressive_fmha.py:119-151 (pos_emb=True). drop: the embedding Dropout (:139) as an explicit
+    multiplier, None = identity."""
     x = p[f"{prefix}/x_embedding/embeddings"][torch.as_tensor(tokens)]
     if y_cond is not None:
         x = torch.cat([torch.as_tensor(y_cond, dtype=x.dtype), x[:, 1:]], dim=1)
     x = x * math.sqrt(cfg.width)
     x = x + p[f"{prefix}/pos_embedding/embeddings"][:x.shape[1]].unsqueeze(0)
+    if drop is not None:
+        x = x * drop
     if x_cond is not None:
         x = x + torch.as_tensor(x_cond, dtype=x.dtype)[:, :x.shape[1]]
     return x
 
 
-def model_forward(p, cfg: PriorConfig, tokens, prefix="prior", y_cond=None, x_cond=None):
-    """(N, T) tokens -> (N, T, bins) logits."""
-    x = embed(p, cfg, tokens, prefix, y_cond, x_cond)
+def model_forward(p, cfg: PriorConfig, tokens, prefix="prior", y_cond=None, x_cond=None, drop=None):
+    """(N, T) tokens -> (N, T, bins) logits. drop: {"emb": mask, "layer{i}": mask} dropout multipliers."""
+    drop = drop or {}
+    x = embed(p, cfg, tokens, prefix, y_cond, x_cond, drop.get("emb"))
     for layer in range(cfg.depth):
-        x = res_attn_block(p, f"{prefix}/layer{layer}", x, cfg.attn_func(layer), cfg.block_len)
+        x = res_attn_block(p, f"{prefix}/layer{layer}", x, cfg.attn_func(layer), cfg.block_len,
+                           drop.get(f"layer{layer}"))
     return x @ p[f"{prefix}/out/kernel"] + p[f"{prefix}/out/bias"]
 
 
@@ -250,17 +259,27 @@ def shift_right(codes, start_token):
     return torch.cat([torch.full_like(c[:, :1], start_token), c[:, :-1]], dim=1)
 
 
-def train_step_grads(p, cfg: PriorConfig, codes, tf_mask, prefix="prior", x_cond=None):
+def train_step_grads(p, cfg: PriorConfig, codes, tf_mask, prefix="prior", x_cond=None, labels=None, drop1=None,
+                     drop2=None):
     """prior.py:272-300: forward once, argmax -> shifted predictions, mix with the shifted codes where tf_mask
-    (= uniform < teacher_force_rate), forward again with gradients. Returns (loss, accuracy, grads, batch_input)."""
+    (= uniform < teacher_force_rate), forward again with gradients. Returns (loss, accuracy, grads, batch_input).
+    labels = (table name, y): the LabelConditioner's rows (label_conditioners.py:26-45) replace position 0 and
+    are trained with the prior (prior.py:268-271,299). drop1 / drop2: the two passes' dropout multipliers."""
     start = cfg.bins - 1
     latent_input = shift_right(codes, start)
+
+    def ycond(q):
+        if labels is None:
+            return None
+        name, y = labels
+        return q[name][torch.as_tensor(y)].unsqueeze(1)
+
     with torch.no_grad():
-        logits0 = model_forward(p, cfg, latent_input, prefix, x_cond=x_cond)
+        logits0 = model_forward(p, cfg, latent_input, prefix, y_cond=ycond(p), x_cond=x_cond, drop=drop1)
     pred = shift_right(argmax_lowest(logits0), start)
     batch_input = torch.where(torch.as_tensor(tf_mask), pred, latent_input)
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = model_forward(leaves, cfg, batch_input, prefix, x_cond=x_cond)
+    logits = model_forward(leaves, cfg, batch_input, prefix, y_cond=ycond(leaves), x_cond=x_cond, drop=drop2)
     loss = ce_loss(codes, logits)
     loss.backward()
     grads = {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in leaves.items()}
@@ -294,14 +313,14 @@ def gumbel_noise(seed: int, n: int, step: int, bins: int) -> np.ndarray:
 
 
 def sample_full_recompute(p, cfg: PriorConfig, n_samples: int, max_length: int, seed: int, prefix="prior",
-                          x_cond=None):
+                          x_cond=None, y_cond=None):
     """autoregressive_fmha.py:162-240: start token, then max_length steps of a FULL forward over the prefix,
     last-position logits + Gumbel noise (RelaxedOneHotCategorical(1).sample() then argmax = argmax(logits + G)).
     Returns (N, max_length + 1) int64 tokens and the per-step top-2 margins of logits + G."""
     out = torch.full((n_samples, 1), cfg.bins - 1, dtype=torch.int64)
     margins = np.zeros((n_samples, max_length))
     for i in range(max_length):
-        logits = model_forward(p, cfg, out, prefix, x_cond=x_cond)[:, -1]          # (N, bins)
+        logits = model_forward(p, cfg, out, prefix, y_cond=y_cond, x_cond=x_cond)[:, -1]  # (N, bins)
         g = torch.from_numpy(np.stack([gumbel_noise(seed, n, i, cfg.bins) for n in range(n_samples)])).to(logits.dtype)
         z = logits + g
         top2 = torch.topk(z, 2, dim=-1).values

@@ -378,10 +378,107 @@ def test_upsampler_train_step_with_conditioner_matches_oracle(cuda):
     res = pr.train_step((codes.cuda(), upper.cuda()), tf_mask=mask.cuda())
     torch.cuda.synchronize()
     assert torch.equal(pr._last_batch_input.cpu(), bi)
-    assert abs(float(res["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
+    loss = float(loss.detach())
+    assert abs(float(res["loss"]) - loss) <= 1e-5 * abs(loss)
     got = pr.prior.store.grads()
     gmax = max(float(t.grad.abs().max()) for t in pt.values() if t.grad is not None)
     for k, t in pt.items():
         ref = t.grad if t.grad is not None else torch.zeros_like(t)
         err = float((torch.from_numpy(got[k]).double() - ref).abs().max()) / max(float(ref.abs().max()), 1e-4 * gmax)
         assert err < 5e-4, (k, err)
+
+
+# ------------------------------------------------------------------ dropout and label conditioning in training
+def _dropout_masks(pr, N, T, seed_pass, ctr):
+    """The product's dropout multipliers for one pass (embedding: salt VQA_EMB_DROPOUT_SALT over (N, T, W); layer i:
+    salt 1000 + i over the attention output), read back by dropping out a tensor of ones."""
+    import vqa_lib as V
+    m = pr.prior
+    out = {}
+    ones = torch.ones(N, T, m.d_model, device="cuda")
+    e = ones.clone()
+    V.dropout_(e, m.rate, seed_pass, V.EMB_DROPOUT_SALT, ctr)
+    out["emb"] = e.double().cpu()
+    for i in range(m.depth):
+        t = ones.clone()
+        V.dropout_(t, m.rate, seed_pass, 1000 + i, ctr)
+        out[f"layer{i}"] = t.double().cpu()
+    return out
+
+
+def _grad_errs(got, grads):
+    gmax = max(float(g.abs().max()) for g in grads.values())
+    errs = {k: float((torch.from_numpy(got[k]).double() - grads[k].double()).abs().max()) /
+            max(float(grads[k].abs().max()), 1e-4 * gmax) for k in grads}
+    worst = max(errs, key=errs.get)
+    return worst, errs[worst]
+
+
+@pytest.mark.parametrize("labels", [False, True])
+def test_train_step_dropout_and_labels_match_oracle(cuda, labels):
+    """drop_out_rate 0.1 in both teacher-forcing passes (embedding and attention-output dropout, the masks read back
+    from the product's counter-based RNG) and, with labels, the LabelConditioner: genre rows replace position 0
+    (autoregressive_fmha.py:120-129) and the genre table is trained with the prior (prior.py:268-271,299). Loss,
+    accuracy, pass-1 mixing and every gradient (the genre table's included) vs fp64 autograd."""
+    from prior import Prior
+    cfg = CFG
+    pk = dict(width=cfg.width, depth=cfg.depth, heads=cfg.heads, blocks=cfg.blocks, attn_stacks=cfg.attn_stacks,
+              drop_out_rate=0.1)
+    pr = Prior(0, [(cfg.ctx,)], cfg.bins, [3], [2], None, pk, None, genre_classes=10 if labels else None,
+               dtype="fp32", device="cuda", seed=11)
+    vals = pr.prior.store.values()
+    g = _gen(17)
+    N = 2
+    codes = torch.randint(0, cfg.bins - 1, (N, cfg.ctx), generator=g)
+    mask = torch.rand(N, cfg.ctx, generator=g) < 0.2
+    y = torch.tensor([3, 7])
+    ctr = pr.optimizer.iterations.clone()
+    seed = pr.teacher_seed
+    d1 = _dropout_masks(pr, N, cfg.ctx, seed * 7919 + 1, ctr)
+    d2 = _dropout_masks(pr, N, cfg.ctx, seed * 7919 + 2, ctr)
+    lab = ("label_conditioner/genre_embedding/embeddings", y) if labels else None
+    loss, acc, grads, bi = P.train_step_grads(P.to_torch(vals), cfg, codes, mask, labels=lab, drop1=d1, drop2=d2)
+    x = (codes.cuda(), y.cuda()) if labels else codes.cuda()
+    res = pr.train_step(x, tf_mask=mask.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(pr._last_batch_input.cpu(), bi)
+    assert abs(float(res["loss"]) - loss) <= 1e-5 * abs(loss)
+    assert abs(float(res["accuracy"]) - acc) <= 1.0 / codes.numel() + 1e-7
+    got = pr.prior.store.grads()
+    if labels:
+        gl = grads[lab[0]]
+        assert float(gl[3].abs().max()) > 0 and float(gl[0].abs().max()) == 0  # only the rows of the labels
+    worst, err = _grad_errs(got, grads)
+    assert err < 2e-4, (worst, err)
+
+
+def test_conditioned_labelled_graph_replay_matches_eager(cuda):
+    """The upsampler (ConditionerNet on the level above) with genre labels and dropout 0.1, captured as one hipGraph:
+    replays (the teacher-forcing draw and the dropout masks advancing on the device counter) end bitwise where the
+    same steps run eagerly end."""
+    from prior import Prior
+    ck = dict(dilation_factor=3, dilation_cycle=4, residual_width=32, residual_depth=8)
+    pk = dict(width=128, depth=3, heads=2, blocks=4, attn_stacks=1, drop_out_rate=0.1)
+
+    def make():
+        return Prior(0, [(256,), (64,)], 64, [3, 2], [2, 2], None, pk, ck, genre_classes=10, dtype="fp32",
+                     device="cuda", seed=5)
+
+    a, b = make(), make()
+    g = _gen(23)
+    codes = torch.randint(0, 63, (2, 256), generator=g).cuda()
+    upper = torch.randint(0, 63, (2, 64), generator=g).cuda()
+    y = torch.tensor([1, 8]).cuda()
+    for _ in range(3):
+        a.train_step((codes, upper, y))
+    b.capture_train_step((codes, upper, y), warmup=1)
+    b.train_step((codes, upper, y))
+    b.train_step((codes, upper, y))
+    torch.cuda.synchronize()
+    assert torch.equal(a.prior.store.flat, b.prior.store.flat)
+    assert float(a.results()["loss"]) == float(b.results()["loss"])
+    # the genre rows of the labels moved, the others did not
+    lc = a.label_conditioner
+    w = a.prior.store.view(lc.name)
+    w0 = make().prior.store.view(lc.name)
+    assert not torch.equal(w[1], w0[1]) and torch.equal(w[0], w0[0])

@@ -390,6 +390,8 @@ __global__ __launch_bounds__(256) void seqlin_wgrad_kernel(SeqWgArgs a) {
 // ---------------------------------------------------------------------------------------------------
 // embeddings (autoregressive_fmha.py:119-151): x = table[tok] (row 0 replaced by y_cond when given) * scale
 // + pos[t]; dropout; + x_cond. One thread per 4 channels.
+constexpr unsigned long long kEmbDropSalt = 0x454d42ull;  // VQA_EMB_DROPOUT_SALT (vqa.h)
+
 struct EmbArgs {
   const float* table;
   const float* pos;
@@ -426,10 +428,12 @@ __global__ __launch_bounds__(256) void prior_embed_kernel(EmbArgs a) {
     v = v * a.scale;
     v = v + *(const f32x4*)(a.pos + (long long)t * a.W + c);
     if (a.rate > 0.f) {
+      // the mask of dropout_kernel over the flat (N, T, W) index with salt kEmbDropSalt: the backward is
+      // vqa_dropout on the gradient with the same (seed, salt, counter)
       const float ks = 1.0f / (1.0f - a.rate);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = prior_uniform(seed, 0x454d42ull, (uint64_t)r, (uint64_t)(c + i)) >= a.rate
-                                             ? v[i] * ks : 0.f;
+      for (int i = 0; i < 4; ++i)
+        v[i] = prior_uniform(seed, kEmbDropSalt, (uint64_t)(r * a.W + c + i), 0) >= a.rate ? v[i] * ks : 0.f;
     }
     if (a.xcond) v = v + ld4((const T*)a.xcond + r * a.W + c);
     st4((T*)a.out + r * a.W + c, v);

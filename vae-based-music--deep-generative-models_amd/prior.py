@@ -270,7 +270,7 @@ class FMHABasedAutoregressiveModel:
     def __init__(self, target_vocab_size, width, depth, blocks, m_attn=0.25, m_mlp=1.0, heads=1, attn_stacks=1,
                  maximum_pos_encoding=5000, drop_out_rate=0.1, context_length=None, zq_shapes=None, level=0, levels=3,
                  pos_emb=True, downs=None, strides=None, cond_kwargs=None, dtype="fp32", device="cuda", seed=1,
-                 store: Optional[ParamStore] = None, prefix="prior", grad_extra: int = 0, **kwargs):
+                 store: Optional[ParamStore] = None, prefix="prior", grad_extra: int = 0, label_bins=None, **kwargs):
         self.context_length = int(np.prod(context_length))
         self.bins, self.d_model, self.depth = target_vocab_size, width, depth
         self.heads, self.blocks = heads, blocks
@@ -301,6 +301,12 @@ class FMHABasedAutoregressiveModel:
         self.out_bias = st.add(f"{prefix}/out/bias", (self.bins,), "zeros")
         if self.conditioner is not None:
             self.conditioner.build(st, f"{prefix}/conditioner", width, self.cdt)
+        # prior.py:154-157: the Prior's LabelConditioner (genre embedding -> position 0), in the same store so
+        # that Adam and the data-parallel bucket cover it
+        self.label_conditioner = None
+        if label_bins is not None:
+            self.label_conditioner = LabelConditioner(label_bins, width)
+            self.label_conditioner.build(st, "label_conditioner")
         if own:
             # the gradient buffer is the head of the data-parallel bucket: grad_extra trailing slots for scalars
             st.materialize(self.device, grad_buffer=torch.zeros(st.size + grad_extra, device=self.device), seed=seed)
@@ -412,6 +418,8 @@ class FMHABasedAutoregressiveModel:
                        self.start_token, seed, ycond=self._ycond(y_cond), xcond=xc, forced=forced, logits=logits)
         if return_logits:
             return tokens, logits
+        if return_attention_weights:
+            return tokens, {}  # the decode kernel keeps no attention-weight tensors
         return tokens
 
     @property
@@ -440,16 +448,15 @@ class Prior:
             heads=prior_kwargs["heads"], blocks=prior_kwargs["blocks"], attn_stacks=prior_kwargs["attn_stacks"],
             drop_out_rate=prior_kwargs.get("drop_out_rate", 0.1), context_length=self.z_shape, zq_shapes=z_shapes,
             level=level, levels=self.levels, downs=down_depth, strides=strides, cond_kwargs=x_cond_kwargs,
-            dtype=dtype, device=device, seed=seed, grad_extra=2)
+            dtype=dtype, device=device, seed=seed, grad_extra=2, label_bins=genre_classes)
         # data parallel (one process per GPU): ONE all_reduce per step over [gradients | loss, accuracy]
         self.process_group = process_group
         st = self.prior.store
         self.bucket = st.grad
         self._scalars = self.bucket[st.size:st.size + 2]
         self.label_conditioner = None
-        if genre_classes is not None:
-            raise NotImplementedError("label-conditioned training (LabelConditioner) is not built yet; the sampler "
-                                      "takes y_cond")
+        # prior.py:154-157 (LabelConditioner(genre_bins, width)): built into the prior's parameter store
+        self.label_conditioner = self.prior.label_conditioner
         self.optimizer = Adam(learning_rate=learning_rate)
         self.optimizer.build(self.prior.store)  # its device step counter also drives dropout / teacher forcing
         self.train_loss_tracker = Mean("train_loss", self.device)
@@ -479,22 +486,35 @@ class Prior:
         return zs[self.level + 1][:, start // r:end // r]
 
     def _codes(self, x):
-        """Raw audio (N, T, 1) -> the VQ-VAE's codes of this level (and of the level above for the upsampler
-        conditioning, prior.py:257-260); int64 codes are taken as they are, as (codes, upper_codes) when the prior
-        is conditioned on the level above."""
+        """-> (codes (N, T_l) int64, upper-level codes or None, labels (N,) int64 or None).
+
+        x is raw audio (N, T, 1) (encoded with `vqvae_model`: this level's codes and, for the upsampler
+        conditioning, the level above's, prior.py:257-260) or the codes themselves (int64). A tuple carries the
+        extras: (audio, y) as the reference's train_step takes it (prior.py:251-254), (codes, upper_codes) for a
+        prior conditioned on the level above, (codes, y) / (codes, upper_codes, y) with genre labels."""
+        extras = []
         if isinstance(x, (tuple, list)):
-            first = torch.as_tensor(x[0], device=self.device)
-            if first.dtype == torch.int64 and len(x) > 1 and self.prior.conditioner is not None:
-                return first.contiguous(), torch.as_tensor(x[1], device=self.device).long().contiguous()
-            x = first
+            x, extras = x[0], list(x[1:])
         x = torch.as_tensor(x, device=self.device)
+        conditioned = self.prior.conditioner is not None
         if x.dtype == torch.int64:
-            if self.prior.conditioner is not None:
-                raise ValueError("a conditioned prior needs (codes, upper_level_codes)")
-            return x.contiguous(), None
-        codes = self.vqvae.encode(x, start_level=self.level, end_level=self.levels)
-        upper = codes[1] if self.level != self.levels - 1 else None
-        return codes[0].contiguous(), upper
+            codes, upper = x.contiguous(), None
+            if conditioned:
+                if not extras:
+                    raise ValueError("a conditioned prior needs (codes, upper_level_codes)")
+                upper = torch.as_tensor(extras.pop(0), device=self.device).long().contiguous()
+        else:
+            zs = self.vqvae.encode(x, start_level=self.level, end_level=self.levels)
+            codes = zs[0].contiguous()
+            upper = zs[1] if self.level != self.levels - 1 else None
+        y = None
+        if extras and extras[0] is not None:
+            if self.label_conditioner is None:
+                raise ValueError("labels given to a prior built without genre_classes")
+            y = torch.as_tensor(extras[0], device=self.device).long().reshape(-1).contiguous()
+            if y.numel() != codes.shape[0]:
+                raise ValueError(f"{y.numel()} labels for {codes.shape[0]} sequences")
+        return codes, upper, y
 
     def results(self):
         loss = self.train_loss_tracker.result()
@@ -504,7 +524,17 @@ class Prior:
     def _world(self):
         return vqa_dp.world_size(self.process_group)
 
-    def _compute(self, codes, upper, teacher_force_rate, tf_mask=None):
+    def _label_embed(self, y):
+        """LabelConditioner(y) (label_conditioners.py:26-45) as the (N, width) fp32 rows the embedding kernel puts at
+        position 0."""
+        if y is None:
+            return None
+        lc = self.label_conditioner
+        out = torch.empty(y.numel(), self.prior.d_model, dtype=torch.float32, device=self.device)
+        V.embedding_fwd(lc.store.view(lc.name), y, out)
+        return out
+
+    def _compute(self, codes, upper, teacher_force_rate, tf_mask=None, y=None):
         """Both teacher-forcing passes and the backward: gradients and [loss, accuracy] sums in the bucket."""
         m, st = self.prior, self.prior.store
         N, T = codes.shape
@@ -514,6 +544,7 @@ class Prior:
         ctr = self.optimizer.iterations
         row_offset = vqa_dp.rank(self.process_group) * M
         xc = m._cond(upper, save=True) if upper is not None else None
+        yc = self._label_embed(y)
         m.prep_weights(bwd=True)
         # pass 1: teacher-forced input, argmax of the logits (prior.py:277-282)
         latent = torch.empty_like(codes)
@@ -521,7 +552,7 @@ class Prior:
         wt = m._wt(m.cdt)
         b = st.view(m.out_bias)
         with torch.no_grad():
-            h0 = m.hidden(latent, True, xc, seed=seed * 7919 + 1, counter=ctr, prepped=True)
+            h0 = m.hidden(latent, True, xc, yc, seed=seed * 7919 + 1, counter=ctr, prepped=True)
             lse0 = torch.empty(M, dtype=torch.float32, device=dev)
             amax = torch.empty(N, T, dtype=torch.int64, device=dev)
             V.head_fwd(h0, wt, b, lse0, amax=amax)
@@ -531,7 +562,7 @@ class Prior:
         mask = None if tf_mask is None else torch.as_tensor(tf_mask, device=dev).to(torch.uint8).contiguous()
         V.tf_mix(codes, amax, mask, batch_input, m.start_token, rate=float(teacher_force_rate), seed=seed,
                  counter=ctr, row_offset=row_offset)
-        h = m.hidden(batch_input, True, xc, save=True, seed=seed * 7919 + 2, counter=ctr, prepped=True)
+        h = m.hidden(batch_input, True, xc, yc, save=True, seed=seed * 7919 + 2, counter=ctr, prepped=True)
         lse = torch.empty(M, dtype=torch.float32, device=dev)
         loss_row = torch.empty(M, dtype=torch.float32, device=dev)
         correct = torch.empty(M, dtype=torch.float32, device=dev)
@@ -548,16 +579,28 @@ class Prior:
                        deferred=deferred)
             for ly in reversed(m.transformer.layers):
                 dh = ly.backward(dh, T, deferred, post)
-            # embeddings: x0 = E[tok] * sqrt(d) + pos (+ x_cond)
+            # embeddings: x0 = dropout(E[tok] * sqrt(d) + pos) (+ x_cond), position 0 = the label embedding
+            # when labels are given (autoregressive_fmha.py:119-151)
+            if xc is not None:
+                m.conditioner.backward(dh)
+            if m.rate > 0:  # the embedding dropout's mask, in place (dh is not read again)
+                V.dropout_(dh, m.rate, seed * 7919 + 2, V.EMB_DROPOUT_SALT, ctr)
+            if m.use_pos_embedding:
+                V.colsum(dh, st.grad_view(m.pos_name), N, T * m.d_model, T * m.d_model)
+            gl = None
+            if y is not None:
+                lc = self.label_conditioner
+                gl = st.grad_view(lc.name)
+                gl.zero_()
+                V.embedding_bwd(dh[:, 0, :].contiguous(), y, gl)
+                dh[:, 0, :].zero_()  # the start token's row does not reach the token table
             gt = st.grad_view(m.emb_name)
             gt.zero_()
             V.embedding_bwd(dh, batch_input, gt)
-            if m.use_pos_embedding:
-                V.colsum(dh, st.grad_view(m.pos_name), N, T * m.d_model, T * m.d_model)
-            if xc is not None:
-                m.conditioner.backward(dh)
             deferred.flush()
             V.scale_f32_(gt, math.sqrt(m.d_model))
+            if gl is not None:
+                V.scale_f32_(gl, math.sqrt(m.d_model))
             for dst, extra in post:
                 V.axpy(dst, extra, dst)
         finally:
@@ -577,9 +620,13 @@ class Prior:
 
     def train_step(self, x, teacher_force_rate=0.2, tf_mask=None):
         """prior.py:241-335. tf_mask (N, T) bool overrides the random teacher-forcing draw (parity tests)."""
-        codes, upper = self._codes(x)
-        if self._graph is not None and tf_mask is None and codes.shape == self._graph_codes.shape:
-            self._graph_codes.copy_(codes)
+        codes, upper, y = self._codes(x)
+        if self._graph is not None and tf_mask is None and self._graph_fits(codes, upper, y):
+            self._graph_in[0].copy_(codes)
+            if upper is not None:
+                self._graph_in[1].copy_(upper)
+            if y is not None:
+                self._graph_in[2].copy_(y)
             g1, g2 = self._graph
             g1.replay()
             if g2 is not None:
@@ -587,22 +634,27 @@ class Prior:
                 g2.replay()
             self._step += 1
             return self.results()
-        self._compute(codes, upper, teacher_force_rate, tf_mask)
+        self._compute(codes, upper, teacher_force_rate, tf_mask, y)
         self._exchange()
         self._apply()
         self._step += 1
         return self.results()
 
+    def _graph_fits(self, codes, upper, y):
+        c, u, l = self._graph_in
+        same = lambda a, b: (a is None) == (b is None) and (a is None or a.shape == b.shape)
+        return same(codes, c) and same(upper, u) and same(y, l)
+
     def test_step(self, x):
         """prior.py:337-372: loss / accuracy of the teacher-forced input (no mixing, no update)."""
         m = self.prior
-        codes, upper = self._codes(x)
+        codes, upper, y = self._codes(x)
         N, T = codes.shape
         M = N * T
         with torch.no_grad():
             latent = torch.empty_like(codes)
             V.tf_mix(codes, None, None, latent, m.start_token)
-            h = m.hidden(latent, False, m._cond(upper))
+            h = m.hidden(latent, False, m._cond(upper), self._label_embed(y))
             lse = torch.empty(M, dtype=torch.float32, device=self.device)
             lr, cr = torch.empty_like(lse), torch.empty_like(lse)
             V.head_fwd(h, m._wt(m.cdt), m.store.view(m.out_bias), lse, targets=codes, loss_row=lr, correct=cr)
@@ -612,18 +664,18 @@ class Prior:
         return {"loss": out[0], "perplexity(per word)": torch.exp(out[0]), "accuracy": out[1]}
 
     def capture_train_step(self, codes_example, teacher_force_rate=0.2, warmup=1):
-        """Record the whole step (both passes, backward, Adam, metrics) as one hipGraph — two around the eager
-        all_reduce under data parallelism; later train_step calls with this shape copy the codes in and replay
-        (the teacher-forcing draw advances on the device)."""
-        codes, upper = self._codes(codes_example)
-        if upper is not None:
-            raise NotImplementedError("graph capture of the conditioned prior step")
-        self._graph_codes = codes.clone()
+        """Record the whole step (both passes, the conditioner, backward, Adam, metrics) as one hipGraph — two
+        around the eager all_reduce under data parallelism; later train_step calls with the same shapes copy the
+        codes (upper-level codes, labels) in and replay (the teacher-forcing draw and dropout advance on the
+        device)."""
+        codes, upper, y = self._codes(codes_example)
+        self._graph_in = tuple(None if t is None else t.clone() for t in (codes, upper, y))
+        c, u, l = self._graph_in
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self._compute(self._graph_codes, None, teacher_force_rate)
+                self._compute(c, u, teacher_force_rate, None, l)
                 self._exchange()
                 self._apply()
         torch.cuda.current_stream(self.device).wait_stream(s)
@@ -631,7 +683,7 @@ class Prior:
         pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool):
-            self._compute(self._graph_codes, None, teacher_force_rate)
+            self._compute(c, u, teacher_force_rate, None, l)
             if self._world() == 1:
                 self._apply()
         g2 = None
@@ -643,6 +695,17 @@ class Prior:
         torch.cuda.synchronize(self.device)
 
     def sample(self, n_samples, z_cond=None, y=None, return_attn_weights=False, seed=0):
-        """prior.py:374-400: one window of n_ctx tokens (without the start token)."""
-        out = self.prior.sample(n_samples, x_cond=z_cond, y_cond=y, seed=seed)
-        return out[:, 1:]
+        """prior.py:374-408: one window of n_ctx tokens, the start token first (as FMHABasedAutoregressiveModel.sample
+        returns it; VQVAESampler drops it). y: genre labels (N,) through the LabelConditioner."""
+        if z_cond is not None and int(z_cond.shape[0]) != n_samples:
+            raise ValueError(f"Batch Size not matching, Expected:{n_samples}, Getting: {int(z_cond.shape[0])}")
+        y_cond = None
+        if y is not None:
+            if self.label_conditioner is None:
+                raise ValueError("labels given to a prior built without genre_classes")
+            y = torch.as_tensor(y, device=self.device).long().reshape(-1).contiguous()
+            if y.numel() != n_samples:
+                raise ValueError(f"Batch Size not matching, Expected:{n_samples}, Getting: {y.numel()}")
+            y_cond = self._label_embed(y)
+        return self.prior.sample(n_samples, x_cond=z_cond, y_cond=y_cond, seed=seed,
+                                 return_attention_weights=return_attn_weights)

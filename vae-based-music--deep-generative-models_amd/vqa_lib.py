@@ -613,6 +613,9 @@ def axpy(x, y, z):
     _check(lib().vqa_axpy(ptr(x), ptr(y), ptr(z), x.numel(), dtype_code(x.dtype), stream()), "vqa_axpy")
 
 
+EMB_DROPOUT_SALT = 0x454D42  # VQA_EMB_DROPOUT_SALT: vqa_prior_embed_fwd's dropout mask is vqa_dropout's with this salt
+
+
 def dropout_(x, rate, seed, salt, counter=None):
     _check(lib().vqa_dropout(ptr(x), x.numel(), rate, seed, salt, ptr(counter), dtype_code(x.dtype), stream()),
            "vqa_dropout")
