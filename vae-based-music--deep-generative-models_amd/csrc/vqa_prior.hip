@@ -996,7 +996,53 @@ __device__ __forceinline__ void stage_rows128(T* dst, const T* src, long long ro
   }
 }
 
-// workgroup = 128 rows (wave w: rows 32w .. 32w+31 as two 16-row subtiles); vocab tiles of 64 in LDS
+// 64 rows of HK channels staged HBM -> registers -> LDS: the next tile's loads are issued before the current
+// tile's MFMAs, so their latency hides behind them (rows past `avail` are zeros)
+template <class T>
+struct Rows64Regs {
+  static constexpr int VEC = 16 / (int)sizeof(T), CPR = HK / VEC, PER = 64 * CPR / 256, S = hstride<T>();
+  uint4 v[PER];
+  __device__ __forceinline__ void load(const T* src, long long row0, long long avail) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + i * 256, j = e / CPR, q = e - j * CPR;
+      v[i] = row0 + j < avail ? *(const uint4*)(src + (row0 + j) * HK + q * VEC) : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(T* dst) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + i * 256, j = e / CPR, q = e - j * CPR;
+      *(uint4*)(dst + j * S + q * VEC) = v[i];
+    }
+  }
+};
+
+// logits^T of a 16-vocab subtile with the 16 rows' fragments held in registers (xf[kc] = rows' K slice kc)
+template <class T>
+__device__ __forceinline__ f32x4 head_tile_x(const T* wtl, const typename Mfma<T>::frag (&xf)[HK / Mfma<T>::KS],
+                                             int stride) {
+  typedef Mfma<T> M;
+  const int lane = threadIdx.x & 63, kof = M::koff(lane), col = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kc = 0; kc < HK / M::KS; ++kc) acc = M::mma(M::load(wtl + col * stride + kof + kc * M::KS), xf[kc], acc);
+  return acc;
+}
+
+// the B fragments of a workgroup's rows (wave w: rows 32w + 16s + (lane & 15)) for every K slice
+template <class T>
+__device__ __forceinline__ void head_xfrags(typename Mfma<T>::frag (&xf)[2][HK / Mfma<T>::KS], const T* X, int stride) {
+  typedef Mfma<T> M;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, kof = M::koff(lane), col = lane & 15;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int kc = 0; kc < HK / M::KS; ++kc) xf[s][kc] = M::load(X + (wave * 32 + s * 16 + col) * stride + kof + kc * M::KS);
+}
+
+// workgroup = 128 rows (wave w: rows 32w .. 32w+31 as two 16-row subtiles, their fragments in registers);
+// vocab tiles of 64 through LDS, the next one prefetched into registers
 template <class T>
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   constexpr int S = hstride<T>();
@@ -1006,6 +1052,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   const long long r0 = (long long)blockIdx.x * 128;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   stage_rows128<T>(X, (const T*)a.x, r0, a.M, 128);
+  Rows64Regs<T> wn;
+  wn.load((const T*)a.wt, 0, a.V);
+  __syncthreads();
+  typename Mfma<T>::frag xf[2][HK / Mfma<T>::KS];
+  head_xfrags<T>(xf, X, S);
   long long rows[2];
   int64_t tg[2];
   float m[2], l[2], bv[2], tl[2];
@@ -1018,14 +1069,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   }
   for (int v0 = 0; v0 < a.V; v0 += 64) {
     __syncthreads();
-    stage_rows128<T>(W, (const T*)a.wt, v0, a.V, 64);
+    wn.store(W);
+    if (v0 + 64 < a.V) wn.load((const T*)a.wt, v0 + 64, a.V);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float x[4][4], mt = -INFINITY;
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
-        const f32x4 acc = head_tile<T>(W + st * 16 * S, X + (wave * 32 + s * 16) * S, S);
+        const f32x4 acc = head_tile_x<T>(W + st * 16 * S, xf[s], S);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int v = v0 + st * 16 + 4 * g + i;
@@ -1079,6 +1131,11 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
   const long long r0 = (long long)blockIdx.x * 128;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   stage_rows128<T>(X, (const T*)a.x, r0, a.M, 128);
+  Rows64Regs<T> wn;
+  wn.load((const T*)a.wt, 0, a.V);
+  __syncthreads();
+  typename Mfma<T>::frag xf[2][HK / Mfma<T>::KS];
+  head_xfrags<T>(xf, X, S);
   long long rows[2];
   int64_t tg[2];
   float lse[2];
@@ -1094,14 +1151,15 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
   }
   for (int v0 = 0; v0 < a.V; v0 += 64) {
     __syncthreads();
-    stage_rows128<T>(W, (const T*)a.wt, v0, a.V, 64);
+    wn.store(W);
+    if (v0 + 64 < a.V) wn.load((const T*)a.wt, v0 + 64, a.V);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dl[4][4];
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
-        const f32x4 z = head_tile<T>(W + st * 16 * S, X + (wave * 32 + s * 16) * S, S);
+        const f32x4 z = head_tile_x<T>(W + st * 16 * S, xf[s], S);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int v = v0 + st * 16 + 4 * g + i;
@@ -1150,14 +1208,31 @@ __global__ __launch_bounds__(256) void head_bwd_dw_kernel(HeadArgs a) {
   for (int kt = 0; kt < HK / 16; ++kt) acc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db = 0.f;
   const int kof = M::koff(lane);
-  for (long long c0 = rb; c0 < re; c0 += 64) {
-    __syncthreads();
-    stage_rows128<T>(X, (const T*)a.x, c0, re, 64);
+  // the next row tile (and its lse / targets) prefetched into registers during the current one's MFMAs
+  Rows64Regs<T> xn;
+  float ln = INFINITY;
+  int64_t tn = -1;
+  auto fetch = [&](long long c0) {
+    xn.load((const T*)a.x, c0, re);
     if (threadIdx.x < 64) {
       const bool in = c0 + threadIdx.x < re;
-      Ls[threadIdx.x] = in ? a.lse[c0 + threadIdx.x] : INFINITY;
-      Tg[threadIdx.x] = in ? a.tgt[c0 + threadIdx.x] : -1;
+      ln = in ? a.lse[c0 + threadIdx.x] : INFINITY;
+      tn = in ? a.tgt[c0 + threadIdx.x] : -1;
     }
+  };
+  if (rb < re) fetch(rb);
+  __syncthreads();
+  typename M::frag wf[HK / M::KS];  // this wave's 16 vocab columns, every K slice
+#pragma unroll
+  for (int kc = 0; kc < HK / M::KS; ++kc) wf[kc] = M::load(W + (wave * 16 + li) * S + kof + kc * M::KS);
+  for (long long c0 = rb; c0 < re; c0 += 64) {
+    __syncthreads();
+    xn.store(X);
+    if (threadIdx.x < 64) {
+      Ls[threadIdx.x] = ln;
+      Tg[threadIdx.x] = tn;
+    }
+    if (c0 + 64 < re) fetch(c0 + 64);
     __syncthreads();
     float dl[4][4];
 #pragma unroll
@@ -1165,8 +1240,7 @@ __global__ __launch_bounds__(256) void head_bwd_dw_kernel(HeadArgs a) {
       // logits[row][v]: A = X rows (rs*16 + col), B = W^T (vocab col)
       f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kc = 0; kc < HK; kc += M::KS)
-        z = M::mma(M::load(X + (rs * 16 + li) * S + kof + kc), M::load(W + (wave * 16 + li) * S + kof + kc), z);
+      for (int kc = 0; kc < HK / M::KS; ++kc) z = M::mma(M::load(X + (rs * 16 + li) * S + kof + kc * M::KS), wf[kc], z);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = rs * 16 + 4 * g + i;
