@@ -1030,6 +1030,26 @@ __device__ __forceinline__ f32x4 head_tile_x(const T* wtl, const typename Mfma<T
   return acc;
 }
 
+// this lane's share of dot(row, w) for a row held as B fragments (xf[kc]: channels kc*KS + koff ..) and a
+// (HK) row w of Wt in the activation dtype; grp_sum over the four lane groups completes it
+template <class T>
+__device__ __forceinline__ float head_dot_row(const typename Mfma<T>::frag (&xf)[HK / Mfma<T>::KS], const T* w) {
+  typedef Mfma<T> M;
+  const int kof = M::koff(threadIdx.x & 63);
+  float acc = 0.f;
+#pragma unroll
+  for (int kc = 0; kc < HK / M::KS; ++kc) {
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 wv = *(const bf16x8*)(w + kc * M::KS + kof);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = __builtin_fmaf((float)xf[kc][j], (float)wv[j], acc);
+    } else {
+      acc = __builtin_fmaf(xf[kc], w[kc * M::KS + kof], acc);
+    }
+  }
+  return acc;
+}
+
 // the B fragments of a workgroup's rows (wave w: rows 32w + 16s + (lane & 15)) for every K slice
 template <class T>
 __device__ __forceinline__ void head_xfrags(typename Mfma<T>::frag (&xf)[2][HK / Mfma<T>::KS], const T* X, int stride) {
@@ -1067,37 +1087,61 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
     tg[s] = (a.tgt && rows[s] < a.M) ? a.tgt[rows[s]] : -1;
     m[s] = -INFINITY; l[s] = 0.f; bv[s] = -INFINITY; bi[s] = 0; tl[s] = -INFINITY;
   }
+  constexpr float L2E = 1.4426950408889634f;
   for (int v0 = 0; v0 < a.V; v0 += 64) {
     __syncthreads();
     wn.store(W);
     if (v0 + 64 < a.V) wn.load((const T*)a.wt, v0 + 64, a.V);
+    // this lane's 16 vocab slots of the tile: v0 + 16 st + 4 g + i (slots past V: -inf)
+    f32x4 bq[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int vb = v0 + st * 16 + 4 * g;
+      if (vb + 4 <= a.V) {
+        bq[st] = *(const f32x4*)(a.bias + vb);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bq[st][i] = vb + i < a.V ? a.bias[vb + i] : -INFINITY;
+      }
+    }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float x[4][4], mt = -INFINITY;
+      float x[16];
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const f32x4 acc = head_tile_x<T>(W + st * 16 * S, xf[s], S);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int v = v0 + st * 16 + 4 * g + i;
-          const float z = v < a.V ? acc[i] + a.bias[v] : -INFINITY;
-          x[st][i] = z;
-          mt = fmaxf(mt, z);
-          if (z > bv[s]) { bv[s] = z; bi[s] = v; }  // vocab ascends within the lane: first maximum kept
-          if (v == tg[s]) tl[s] = z;
-        }
+        for (int i = 0; i < 4; ++i) x[4 * st + i] = acc[i] + bq[st][i];  // -inf past V
+      }
+      float mt = x[0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) mt = fmaxf(mt, x[k]);
+      // the first slot holding the tile maximum (slots ascend in vocab within the lane): tf.argmax's first max
+      int ti = 15;
+#pragma unroll
+      for (int k = 14; k >= 0; --k) ti = x[k] == mt ? k : ti;
+      if (mt > bv[s]) {
+        bv[s] = mt;
+        bi[s] = v0 + (ti >> 2) * 16 + 4 * g + (ti & 3);
       }
       const float mn = fmaxf(m[s], mt);
       if (mn == -INFINITY) continue;  // only vocab slots past V in this lane so far
+      const float nm = -mn * L2E;
       float ps = 0.f;
 #pragma unroll
-      for (int st = 0; st < 4; ++st)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ps += __expf(x[st][i] - mn);
-      l[s] = l[s] * __expf(m[s] - mn) + ps;
+      for (int k = 0; k < 16; ++k) ps += __builtin_amdgcn_exp2f(__builtin_fmaf(x[k], L2E, nm));
+      l[s] = l[s] * __builtin_amdgcn_exp2f((m[s] - mn) * L2E) + ps;
       m[s] = mn;
     }
+  }
+  // the target's logit, once per row: the row's fragments (registers) . Wt[target] + bias[target]
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bool tin = tg[s] >= 0 && tg[s] < a.V;
+    const float part = tin ? head_dot_row<T>(xf[s], (const T*)a.wt + tg[s] * HK) : 0.f;
+    const float dot = grp_sum(part);
+    tl[s] = tin ? dot + a.bias[tg[s]] : -INFINITY;
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1110,7 +1154,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
       const int oi = __shfl_xor(bi[s], o, 64);
       if (ov > bv[s] || (ov == bv[s] && oi < bi[s])) { bv[s] = ov; bi[s] = oi; }
     }
-    const float t = grp_max(tl[s]);
+    const float t = tl[s];
     if (g == 0 && rows[s] < a.M) {
       const float lse = mx + logf(lt);
       a.lse[rows[s]] = lse;
@@ -1149,6 +1193,12 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
 #pragma unroll
     for (int kt = 0; kt < HK / 16; ++kt) acc[s][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  // softmax * inv_count = exp2((z + b) log2e - (lse log2e - log2 inv_count)); the target's -inv_count is added
+  // once per row after the loop (dX -= inv_count Wt[target])
+  constexpr float L2E = 1.4426950408889634f;
+  float nl[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) nl[s] = -(lse[s] * L2E - __log2f(a.inv_count));
   for (int v0 = 0; v0 < a.V; v0 += 64) {
     __syncthreads();
     wn.store(W);
@@ -1160,13 +1210,16 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const f32x4 z = head_tile_x<T>(W + st * 16 * S, xf[s], S);
+        const int vb = v0 + st * 16 + 4 * g;
+        f32x4 bq;  // slots past V: -inf (probability 0)
+        if (vb + 4 <= a.V) {
+          bq = *(const f32x4*)(a.bias + vb);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int v = v0 + st * 16 + 4 * g + i;
-          float d = v < a.V ? __expf(z[i] + a.bias[v] - lse[s]) : 0.f;
-          if (v == tg[s]) d -= 1.f;
-          dl[st][i] = d * a.inv_count;
+          for (int i = 0; i < 4; ++i) bq[i] = vb + i < a.V ? a.bias[vb + i] : -INFINITY;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dl[st][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(z[i] + bq[i], L2E, nl[s]));
       }
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
@@ -1180,8 +1233,14 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     if (rows[s] >= a.M) continue;
+    const bool tin = tg[s] >= 0 && tg[s] < a.V;
+    const T* wtg = (const T*)a.wt + (tin ? tg[s] : 0) * HK;
 #pragma unroll
-    for (int kt = 0; kt < HK / 16; ++kt) st4((T*)a.dx + rows[s] * HK + kt * 16 + 4 * g, acc[s][kt]);
+    for (int kt = 0; kt < HK / 16; ++kt) {
+      f32x4 o = acc[s][kt];
+      if (tin) o = o - ld4(wtg + kt * 16 + 4 * g) * a.inv_count;  // the one-hot term of dlogits
+      st4((T*)a.dx + rows[s] * HK + kt * 16 + 4 * g, o);
+    }
   }
 }
 
@@ -1195,13 +1254,15 @@ __global__ __launch_bounds__(256) void head_bwd_dw_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* W = (T*)smem;     // [64][S]
   T* X = W + 64 * S;   // [64][S]
-  __shared__ float Ls[64];
-  __shared__ int64_t Tg[64];
+  __shared__ __attribute__((aligned(16))) float Ls[64];  // lse log2e - log2 inv_count (+inf past the segment)
+  __shared__ __attribute__((aligned(16))) int Tg[64];     // targets (-1 past the segment)
   const int nvt = (a.V + 63) / 64, vt = blockIdx.x % nvt, seg = blockIdx.x / nvt, v0 = vt * 64;
   const long long rb = (long long)seg * a.seg_rows, re = std::min<long long>(a.M, rb + a.seg_rows);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   const int v = v0 + wave * 16 + li;
-  const float bias = v < a.V ? a.bias[v] : 0.f;
+  constexpr float L2E = 1.4426950408889634f;
+  const float bl = v < a.V ? a.bias[v] * L2E : -INFINITY;  // vocab slots past V: probability 0
+  const float l2inv = __log2f(a.inv_count);
   stage_rows128<T>(W, (const T*)a.wt, v0, a.V, 64);
   f32x4 acc[HK / 16];
 #pragma unroll
@@ -1211,13 +1272,13 @@ __global__ __launch_bounds__(256) void head_bwd_dw_kernel(HeadArgs a) {
   // the next row tile (and its lse / targets) prefetched into registers during the current one's MFMAs
   Rows64Regs<T> xn;
   float ln = INFINITY;
-  int64_t tn = -1;
+  int tn = -1;
   auto fetch = [&](long long c0) {
     xn.load((const T*)a.x, c0, re);
     if (threadIdx.x < 64) {
       const bool in = c0 + threadIdx.x < re;
-      ln = in ? a.lse[c0 + threadIdx.x] : INFINITY;
-      tn = in ? a.tgt[c0 + threadIdx.x] : -1;
+      ln = in ? a.lse[c0 + threadIdx.x] * L2E - l2inv : INFINITY;
+      tn = in ? (int)a.tgt[c0 + threadIdx.x] : -1;
     }
   };
   if (rb < re) fetch(rb);
@@ -1241,12 +1302,14 @@ __global__ __launch_bounds__(256) void head_bwd_dw_kernel(HeadArgs a) {
       f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < HK / M::KS; ++kc) z = M::mma(M::load(X + (rs * 16 + li) * S + kof + kc * M::KS), wf[kc], z);
+      // rows rs*16 + 4g + i: softmax * inv_count, minus inv_count at the target
+      const f32x4 lq = *(const f32x4*)(Ls + rs * 16 + 4 * g);
+      const int4 tq = *(const int4*)(Tg + rs * 16 + 4 * g);
+      const int tqa[4] = {tq.x, tq.y, tq.z, tq.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int r = rs * 16 + 4 * g + i;
-        float d = v < a.V ? __expf(z[i] + bias - Ls[r]) : 0.f;
-        if (v == Tg[r]) d -= 1.f;
-        d *= a.inv_count;
+        float d = __builtin_amdgcn_exp2f(__builtin_fmaf(z[i], L2E, bl - lq[i]));
+        if (v == tqa[i]) d -= a.inv_count;
         dl[rs][i] = d;
         db += d;
       }
