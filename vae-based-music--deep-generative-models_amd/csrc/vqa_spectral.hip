@@ -28,14 +28,71 @@ __device__ __forceinline__ f32x2 cmul(f32x2 a, f32x2 b) {
 __device__ __forceinline__ f32x2 conj2(f32x2 a) { return f32x2{a.x, -a.y}; }
 __device__ __forceinline__ float cabs2(f32x2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
 
-// One radix-4 Stockham stage at stride S of an N-point transform: x -> y. tw[k] = exp(-2 pi i k / N).
-// TPF threads (local id lt) work on one frame.
+// Mixed-radix Stockham FFT in LDS: radix-8 stages while 8 divides the remaining length, then one radix-4 or
+// radix-2 stage (2048 = 8.8.8.4, 1024 = 8.8.8.2, 512 = 8.8.8: 4 / 4 / 3 passes through LDS instead of the
+// 6 / 5 / 5 of radix 4). Buffers are PADDED: element i lives at pidx(i) = i + i/8, which makes the stride-8
+// writes of the first stage (and the 64-element jumps of the second) bank-conflict-free.
+// tw[k] = exp(-2 pi i k / N) (conjugated for the inverse); TPF threads (local id lt) work on one frame.
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 3); }
+template <int N> constexpr int fpad() { return N + N / 8; }  // padded buffer length (elements)
+
+// y[q + S*(8p + k)] = tw^(k p S) * DFT8_k(x[q + S*(p + r m)], r = 0..7)
+template <int N, int S, bool INV, int TPF>
+__device__ __forceinline__ void fft_stage8(const f32x2* x, f32x2* y, const f32x2* tw, int lt) {
+  constexpr int n = N / S, m = n / 8;
+  constexpr float R2 = 0.70710678118654752f;
+  for (int j = lt; j < N / 8; j += TPF) {
+    const int p = j / S, q = j % S;
+    f32x2 a[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r] = x[pidx(q + S * (p + r * m))];
+    // layer 1 (span 4): u = a_r + a_{r+4}, v = (a_r - a_{r+4}) w8^r
+    f32x2 u[4], v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      u[r] = a[r] + a[r + 4];
+      v[r] = a[r] - a[r + 4];
+    }
+    // w8^1 = (1 -+ i)/sqrt2, w8^2 = -+ i, w8^3 = (-1 -+ i)/sqrt2 (forward / inverse)
+    if (INV) {
+      v[1] = f32x2{R2 * (v[1].x - v[1].y), R2 * (v[1].x + v[1].y)};
+      v[2] = f32x2{-v[2].y, v[2].x};
+      v[3] = f32x2{-R2 * (v[3].x + v[3].y), R2 * (v[3].x - v[3].y)};
+    } else {
+      v[1] = f32x2{R2 * (v[1].x + v[1].y), R2 * (v[1].y - v[1].x)};
+      v[2] = f32x2{v[2].y, -v[2].x};
+      v[3] = f32x2{R2 * (v[3].y - v[3].x), -R2 * (v[3].x + v[3].y)};
+    }
+    // two 4-point DFTs: X[2k'] from u, X[2k'+1] from v
+    f32x2 X[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2* w = h ? v : u;
+      const f32x2 b0 = w[0] + w[2], b1 = w[0] - w[2], b2 = w[1] + w[3], d = w[1] - w[3];
+      const f32x2 jd = INV ? f32x2{-d.y, d.x} : f32x2{d.y, -d.x};
+      X[h] = b0 + b2;
+      X[2 + h] = b1 + jd;
+      X[4 + h] = b0 - b2;
+      X[6 + h] = b1 - jd;
+    }
+    y[pidx(q + S * (8 * p))] = X[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      f32x2 w = tw[k * p * S];
+      if (INV) w = conj2(w);
+      y[pidx(q + S * (8 * p + k))] = cmul(X[k], w);
+    }
+  }
+}
+
+// radix-4 stage (the last one when the remaining length is 4)
 template <int N, int S, bool INV, int TPF>
 __device__ __forceinline__ void fft_stage4(const f32x2* x, f32x2* y, const f32x2* tw, int lt) {
   constexpr int n = N / S, m = n / 4;
   for (int j = lt; j < N / 4; j += TPF) {
     const int p = j / S, q = j % S;
-    const f32x2 a0 = x[q + S * p], a1 = x[q + S * (p + m)], a2 = x[q + S * (p + 2 * m)], a3 = x[q + S * (p + 3 * m)];
+    const f32x2 a0 = x[pidx(q + S * p)], a1 = x[pidx(q + S * (p + m))], a2 = x[pidx(q + S * (p + 2 * m))],
+                a3 = x[pidx(q + S * (p + 3 * m))];
     f32x2 w1 = tw[p * S], w2 = tw[2 * p * S], w3 = tw[3 * p * S];
     if (INV) {
       w1 = conj2(w1);
@@ -44,30 +101,33 @@ __device__ __forceinline__ void fft_stage4(const f32x2* x, f32x2* y, const f32x2
     }
     const f32x2 b0 = a0 + a2, b1 = a0 - a2, b2 = a1 + a3, d = a1 - a3;
     const f32x2 jd = INV ? f32x2{-d.y, d.x} : f32x2{d.y, -d.x};  // +i d (inverse) / -i d (forward)
-    y[q + S * (4 * p)] = b0 + b2;
-    y[q + S * (4 * p + 1)] = cmul(b1 + jd, w1);
-    y[q + S * (4 * p + 2)] = cmul(b0 - b2, w2);
-    y[q + S * (4 * p + 3)] = cmul(b1 - jd, w3);
+    y[pidx(q + S * (4 * p))] = b0 + b2;
+    y[pidx(q + S * (4 * p + 1))] = cmul(b1 + jd, w1);
+    y[pidx(q + S * (4 * p + 2))] = cmul(b0 - b2, w2);
+    y[pidx(q + S * (4 * p + 3))] = cmul(b1 - jd, w3);
   }
 }
 
-// the last stage when log2(N) is odd: n = 2, S = N/2
+// the last stage when the remaining length is 2: n = 2, S = N/2
 template <int N, int TPF>
 __device__ __forceinline__ void fft_stage2(const f32x2* x, f32x2* y, int lt) {
   for (int q = lt; q < N / 2; q += TPF) {
-    const f32x2 a = x[q], b = x[q + N / 2];
-    y[q] = a + b;
-    y[q + N / 2] = a - b;
+    const f32x2 a = x[pidx(q)], b = x[pidx(q + N / 2)];
+    y[pidx(q)] = a + b;
+    y[pidx(q + N / 2)] = a - b;
   }
 }
 
 template <int N, int S, bool INV, int TPF>
 __device__ __forceinline__ void fft_rec(f32x2* x, f32x2* y, const f32x2* tw, int lt) {
   constexpr int n = N / S;
-  if constexpr (n >= 4) {
+  if constexpr (n >= 8) {
+    fft_stage8<N, S, INV, TPF>(x, y, tw, lt);
+    __syncthreads();
+    fft_rec<N, S * 8, INV, TPF>(y, x, tw, lt);
+  } else if constexpr (n == 4) {
     fft_stage4<N, S, INV, TPF>(x, y, tw, lt);
     __syncthreads();
-    fft_rec<N, S * 4, INV, TPF>(y, x, tw, lt);
   } else if constexpr (n == 2) {
     fft_stage2<N, TPF>(x, y, lt);
     __syncthreads();
@@ -76,16 +136,16 @@ __device__ __forceinline__ void fft_rec(f32x2* x, f32x2* y, const f32x2* tw, int
 
 template <int N> constexpr int fft_stages() {
   int s = 0, n = N;
-  while (n >= 4) {
-    n /= 4;
+  while (n >= 8) {
+    n /= 8;
     ++s;
   }
-  return s + (n == 2 ? 1 : 0);
+  return s + (n > 1 ? 1 : 0);
 }
 
-// In-place (logically) N-point FFT of a[] in LDS; b[] is scratch. All frame slots of the workgroup run in
-// lockstep (workgroup barriers). Returns the buffer holding the result (natural order). Unnormalised in
-// both directions. Caller syncs before (a written) — ends with a sync.
+// In-place (logically) N-point FFT of a[] in LDS (padded layout); b[] is scratch. All frame slots of the
+// workgroup run in lockstep (workgroup barriers). Returns the buffer holding the result (natural order,
+// padded). Unnormalised in both directions. Caller syncs before (a written) — ends with a sync.
 template <int N, bool INV, int TPF>
 __device__ __forceinline__ f32x2* fft(f32x2* a, f32x2* b, const f32x2* tw, int lt) {
   fft_rec<N, 1, INV, TPF>(a, b, tw, lt);
@@ -104,8 +164,8 @@ struct SpecFrameArgs {
   int B, T, F, hop, win;
 };
 
-// threads per frame: N/4 butterflies per radix-4 stage, at most the whole workgroup
-template <int N> constexpr int spec_tpf() { return N / 4 < 256 ? N / 4 : 256; }
+// threads per frame: N/8 butterflies per radix-8 stage, at most the whole workgroup
+template <int N> constexpr int spec_tpf() { return N / 8 < 256 ? N / 8 : 256; }
 
 template <int N>
 __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
@@ -116,8 +176,8 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
   float* wn = (float*)(tw + N);
   f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
   const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF;
-  f32x2* buf0 = slots + (size_t)sl * 2 * N;
-  f32x2* buf1 = buf0 + N;
+  f32x2* buf0 = slots + (size_t)sl * 2 * fpad<N>();
+  f32x2* buf1 = buf0 + fpad<N>();
 
   if (a.tw) {
     for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
@@ -151,7 +211,7 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int n = lt + i * TPF;
-      buf0[n] = n < a.win ? f32x2{xv[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
+      buf0[pidx(n)] = n < a.win ? f32x2{xv[i] * wn[n], 0.f} : f32x2{0.f, 0.f};
     }
     if (f0 + gridDim.x * FPI < nframes) load_frame(f0 + gridDim.x * FPI);  // lands during this frame's FFT
     __syncthreads();
@@ -160,7 +220,7 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int k = lt + TPF * j;
-        if (k < KB) a.mag[(size_t)fi * KB + k] = cabs2(X[k]);
+        if (k < KB) a.mag[(size_t)fi * KB + k] = cabs2(X[pidx(k)]);
       }
     }
     __syncthreads();
@@ -193,8 +253,8 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
   float* wn = (float*)(tw + N);
   f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
   const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF, wave = tid >> 6;
-  f32x2* bA = slots + (size_t)sl * 2 * N;
-  f32x2* bB = bA + N;
+  f32x2* bA = slots + (size_t)sl * 2 * fpad<N>();
+  f32x2* bB = bA + fpad<N>();
   __shared__ float red[4][4];
 
   for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
@@ -231,7 +291,7 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int n = lt + i * TPF;
-      bA[n] = n < a.win ? f32x2{ra[i] * wn[n], rb[i] * wn[n]} : f32x2{0.f, 0.f};
+      bA[pidx(n)] = n < a.win ? f32x2{ra[i] * wn[n], rb[i] * wn[n]} : f32x2{0.f, 0.f};
     }
     float mxa[MAG ? 1 : NB], mxb[MAG ? 1 : NB];
     if constexpr (!MAG) {
@@ -252,7 +312,7 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
       if (k < KB) {
         // bins k and N-k of Z are read and (GRAD) rewritten by this thread only: H is built in place
         const int km = (N - k) & (N - 1);
-        const f32x2 zk = Z[k], zm = Z[km];
+        const f32x2 zk = Z[pidx(k)], zm = Z[pidx(km)];
         const f32x2 rka = f32x2{0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
         const f32x2 rkb = f32x2{0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x)};
         const float mra = cabs2(rka), mrb = cabs2(rkb);
@@ -272,10 +332,10 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
             const float gb = mrb > 0.f ? (mrb - mxb[j]) / mrb : 0.f;
             const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
             if (k == 0 || k == N / 2) {
-              Z[k] = f32x2{Ga.x, Gb.x};
+              Z[pidx(k)] = f32x2{Ga.x, Gb.x};
             } else {
-              Z[k] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
-              Z[km] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
+              Z[pidx(k)] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
+              Z[pidx(km)] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
             }
           }
         }
@@ -316,7 +376,7 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
       float* oa = a.out + (size_t)fa * a.win;
       float* ob = a.out + (size_t)fb * a.win;
       for (int n = lt; n < a.win; n += TPF) {
-        const f32x2 y = Y[n];
+        const f32x2 y = Y[pidx(n)];
         if (acta) oa[n] = y.x * wn[n];
         if (actb) ob[n] = y.y * wn[n];
       }
@@ -421,7 +481,7 @@ template <int N>
 static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
   constexpr int FPI = 256 / spec_tpf<N>();
   const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((fa.win + 3) & ~3) * sizeof(float) +
-                     (size_t)FPI * 2 * N * sizeof(f32x2);
+                     (size_t)FPI * 2 * fpad<N>() * sizeof(f32x2);
   const int nframes = fa.B * fa.F;
   const int groups = (nframes + FPI - 1) / FPI;
   const int grid = groups < 2048 ? groups : 2048;
@@ -446,7 +506,7 @@ template <int N, int MODE>
 static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
   constexpr int FPI = 256 / spec_tpf<N>();
   const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((pa.win + 3) & ~3) * sizeof(float) +
-                     (size_t)FPI * 2 * N * sizeof(f32x2);
+                     (size_t)FPI * 2 * fpad<N>() * sizeof(f32x2);
   static size_t lds_set = 0;
   if (lds > 65536 && lds > lds_set) {
     if (hipFuncSetAttribute((const void*)spec_pair_kernel<N, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
