@@ -482,3 +482,37 @@ def test_conditioned_labelled_graph_replay_matches_eager(cuda):
     w = a.prior.store.view(lc.name)
     w0 = make().prior.store.view(lc.name)
     assert not torch.equal(w[1], w0[1]) and torch.equal(w[0], w0[0])
+
+
+def test_prior_checkpoint_resume_bitwise(cuda, tmp_path):
+    """Prior.save / load (weights-only torch checkpoint): 2 steps, save, 2 more steps; a fresh prior loaded from
+    the checkpoint runs the same 2 steps and ends bitwise where the uninterrupted run ended (teacher forcing and
+    dropout follow the restored step counter)."""
+    from prior import Prior
+    ck = dict(dilation_factor=3, dilation_cycle=4, residual_width=32, residual_depth=8)
+    pk = dict(width=128, depth=3, heads=2, blocks=4, attn_stacks=1, drop_out_rate=0.1)
+
+    def make(seed):
+        return Prior(0, [(256,), (64,)], 64, [3, 2], [2, 2], None, pk, ck, genre_classes=10, dtype="fp32",
+                     device="cuda", seed=seed)
+
+    g = _gen(29)
+    batches = [(torch.randint(0, 63, (2, 256), generator=g).cuda(), torch.randint(0, 63, (2, 64), generator=g).cuda(),
+                torch.randint(0, 10, (2,), generator=g).cuda()) for _ in range(4)]
+    a = make(5)
+    for bt in batches[:2]:
+        a.train_step(bt)
+    path = str(tmp_path / "prior.pt")
+    a.save(path)
+    for bt in batches[2:]:
+        a.train_step(bt)
+    b = make(6)  # different init: everything must come from the checkpoint
+    b.load(path)
+    for bt in batches[2:]:
+        b.train_step(bt)
+    torch.cuda.synchronize()
+    assert torch.equal(a.prior.store.flat, b.prior.store.flat)
+    assert torch.equal(a.optimizer.m, b.optimizer.m) and torch.equal(a.optimizer.v, b.optimizer.v)
+    assert float(a.results()["loss"]) == float(b.results()["loss"])
+    raw = torch.load(path, weights_only=True)
+    assert raw["format"] == "vqa-prior/1" and raw["iterations"] == 2

@@ -694,6 +694,40 @@ class Prior:
         self._graph = (g1, g2)
         torch.cuda.synchronize(self.device)
 
+    # -------------------------------------------------------------- checkpoint
+    def save(self, path: str):
+        """Checkpoint to disk (the reference's prior trains under the same injected checkpoint manager as the
+        VQ-VAE, src/callback/monitors.py): tensors, ints and strings only — `torch.load(path, weights_only=True)`
+        reads it. Weights (the ConditionerNet's and the genre table's included), Adam moments and step (the step
+        also drives teacher forcing and dropout), and the loss / accuracy trackers: resuming reproduces the
+        uninterrupted run bit for bit."""
+        st = self.prior.store
+        out = {"format": "vqa-prior/1", "param_names": [n for n, _, _ in st.specs],
+               "config": {"level": self.level, "bins": self.bins, "context_length": self.context_length,
+                          "width": self.prior.d_model, "depth": self.prior.depth, "heads": self.prior.heads,
+                          "blocks": self.prior.blocks, "genre_classes": self.genre_bins},
+               "weights": st.flat.detach().cpu().clone(),
+               "adam_m": self.optimizer.m.detach().cpu().clone(), "adam_v": self.optimizer.v.detach().cpu().clone(),
+               "iterations": int(self.optimizer.iterations.item()), "step": int(self._step),
+               "trackers": torch.stack([t._acc.detach().cpu() for t in self.metrics])}
+        torch.save(out, path)
+
+    def load(self, path: str):
+        """Restore a `save` checkpoint (loaded weights-only: nothing in the file is executed)."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        st = self.prior.store
+        if ck.get("format") != "vqa-prior/1":
+            raise ValueError(f"{path}: not a vqa-prior/1 checkpoint")
+        if ck["param_names"] != [n for n, _, _ in st.specs]:
+            raise ValueError(f"{path}: parameter layout differs from this prior's")
+        st.flat.copy_(ck["weights"].to(self.device))
+        self.optimizer.m.copy_(ck["adam_m"].to(self.device))
+        self.optimizer.v.copy_(ck["adam_v"].to(self.device))
+        self.optimizer.iterations.fill_(int(ck["iterations"]))
+        self._step = int(ck["step"])
+        for t, acc in zip(self.metrics, ck["trackers"]):
+            t._acc.copy_(acc.to(self.device))
+
     def sample(self, n_samples, z_cond=None, y=None, return_attn_weights=False, seed=0):
         """prior.py:374-408: one window of n_ctx tokens, the start token first (as FMHABasedAutoregressiveModel.sample
         returns it; VQVAESampler drops it). y: genre labels (N,) through the LabelConditioner."""
