@@ -104,10 +104,9 @@ template <> __device__ __forceinline__ void st8<float>(float* p, f32x4 lo, f32x4
   *(f32x4*)p = lo;
   *(f32x4*)(p + 4) = hi;
 }
+__device__ __forceinline__ uint4 bf16_bits(f32x4 lo, f32x4 hi);
 template <> __device__ __forceinline__ void st8<bf16>(bf16* p, f32x4 lo, f32x4 hi) {
-  const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
-                    (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
-  *(bf16x8*)p = o;
+  *(uint4*)p = bf16_bits(lo, hi);
 }
 
 // store of the lane's 8 channels through a buffer descriptor: rows past the item's end are dropped by the
@@ -116,9 +115,7 @@ template <class T>
 __device__ __forceinline__ void st8_buf(__amdgpu_buffer_rsrc_t r, int byte_off, f32x4 lo, f32x4 hi) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   if constexpr (sizeof(T) == 2) {
-    const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
-                      (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), r, byte_off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, bf16_bits(lo, hi)), r, byte_off, 0, 0);
   } else {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, lo), r, byte_off, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, hi), r, byte_off + 16, 0, 0);
@@ -164,10 +161,16 @@ template <> __device__ __forceinline__ void pos8<float>(const float* p, bool (&m
 // bf16 epilogue helpers on packed bits (two bf16 per dword, packed integer ops: one instruction per pair)
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
-// the 8 channels rounded to bf16 (v_cvt_pk_bf16_f32), as raw bits
+// two floats rounded to bf16 by ONE v_cvt_pk_bf16_f32 (a vector conversion; element-wise casts of a bf16x8
+// were emitted as one cvt per value plus a v_perm per pair)
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, b2));
+}
+// the 8 channels rounded to bf16, as raw bits
 __device__ __forceinline__ uint4 bf16_bits(f32x4 lo, f32x4 hi) {
-  const bf16x8 o = {(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3], (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
-  return __builtin_bit_cast(uint4, o);
+  return uint4{pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]), pk_bf16(hi[0], hi[1]), pk_bf16(hi[2], hi[3])};
 }
 // d * (r > 0) per bf16 where r >= 0 (a relu'd tensor): d's bits times min(r's bits, 1) (v_pk_min_u16 + v_pk_mul_lo_u16)
 __device__ __forceinline__ unsigned mask_pos_pk(unsigned d, unsigned r) {
