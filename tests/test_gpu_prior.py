@@ -516,3 +516,27 @@ def test_prior_checkpoint_resume_bitwise(cuda, tmp_path):
     assert float(a.results()["loss"]) == float(b.results()["loss"])
     raw = torch.load(path, weights_only=True)
     assert raw["format"] == "vqa-prior/1" and raw["iterations"] == 2
+
+
+def test_train_step_small_prior_full_size(cuda):
+    """The headline prior configuration (BASELINE config 4, SMALL_PRIOR: width 128, depth 6, 2 heads, 4 blocks,
+    ctx 8192, 2048 bins; prior.py:414) on one full-length sequence: fp32 step vs the fp64 oracle (pass-1 mixing
+    exact, loss 1e-5, every gradient 2e-4 of its tensor's max), then the bf16 model's loss within 2e-2 (SURVEY.md
+    §8c) on the same input."""
+    full = P.PriorConfig(bins=2048, ctx=8192, width=128, depth=6, heads=2, blocks=4, attn_stacks=1)
+    pr, vals = _prior(full, seed=13)
+    g = _gen(41)
+    codes = torch.randint(0, full.bins - 1, (1, full.ctx), generator=g)
+    mask = torch.rand(1, full.ctx, generator=g) < 0.2
+    loss, acc, grads, bi = P.train_step_grads(P.to_torch(vals), full, codes, mask)
+    res = pr.train_step(codes.cuda(), tf_mask=mask.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(pr._last_batch_input.cpu(), bi)
+    assert abs(float(res["loss"]) - loss) <= 1e-5 * abs(loss)
+    assert abs(float(res["accuracy"]) - acc) <= 1.0 / codes.numel() + 1e-7
+    worst, err = _grad_errs(pr.prior.store.grads(), grads)
+    assert err < 2e-4, (worst, err)
+    pb, _ = _prior(full, dtype="bf16", seed=13)
+    rb = pb.train_step(codes.cuda(), tf_mask=torch.zeros_like(mask).cuda())
+    l0, _, _, _ = P.train_step_grads(P.to_torch(vals), full, codes, torch.zeros_like(mask))
+    assert abs(float(rb["loss"]) - l0) <= 2e-2 * abs(l0)
