@@ -540,3 +540,20 @@ def test_train_step_small_prior_full_size(cuda):
     rb = pb.train_step(codes.cuda(), tf_mask=torch.zeros_like(mask).cuda())
     l0, _, _, _ = P.train_step_grads(P.to_torch(vals), full, codes, torch.zeros_like(mask))
     assert abs(float(rb["loss"]) - l0) <= 2e-2 * abs(l0)
+
+
+def test_decode_full_context_teacher_forced(cuda):
+    """The decode kernel at the SMALL_UPSAMPLER shape (ctx 8192, 2048 bins, depth 6; BASELINE config 5) with an
+    up-sampled x_cond: teacher-forced logits over 2100 positions (past the first 2048-block boundary, so the
+    prev-row layers attend a real block) vs the fp64 oracle forward, 2e-5 of max |logit|."""
+    full = P.PriorConfig(bins=2048, ctx=8192, width=128, depth=6, heads=2, blocks=4, attn_stacks=1)
+    m, p = _model(full, seed=17)
+    g = _gen(43)
+    L = 2100
+    tok = torch.randint(0, full.bins, (2, L + 1), generator=g)
+    tok[:, 0] = full.bins - 1
+    xc = torch.randn(2, full.ctx, full.width, generator=g) * 0.5
+    _, dl = m.sample(2, max_length=L, x_cond=xc.cuda(), forced=tok.cuda(), return_logits=True, seed=3)
+    torch.cuda.synchronize()
+    ref = P.model_forward(p, full, tok[:, :L], x_cond=xc.double())
+    assert _rel(dl, ref) < 2e-5
