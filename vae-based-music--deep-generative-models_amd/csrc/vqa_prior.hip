@@ -746,7 +746,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   typedef Att<T> A;
   __shared__ __attribute__((aligned(16))) T Qs[64 * AKS];
   __shared__ __attribute__((aligned(16))) T Ds[64 * AKS];  // dO tile
-  __shared__ float Ls[64], Dd[64];
+  __shared__ __attribute__((aligned(16))) float Ls[64];
+  __shared__ __attribute__((aligned(16))) float Dd[64];
   const int kt = blockIdx.x, h = blockIdx.y, n = blockIdx.z, k0 = kt * 64, b = k0 / a.l;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   const int ki = k0 + wave * 16 + li;
@@ -792,13 +793,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
     for (int qs = 0; qs < 4; ++qs) {
       const f32x4 s = A::mm_d(A::ld_d(Qs + (qs * 16 + li) * AKS), kf, f32x4{0.f, 0.f, 0.f, 0.f});
       const f32x4 dp = A::mm_d(A::ld_d(Ds + (qs * 16 + li) * AKS), vf, f32x4{0.f, 0.f, 0.f, 0.f});
+      // the 4 query rows' lse and D: one 16-byte LDS read each
+      const f32x4 lq = *(const f32x4*)(Ls + qs * 16 + 4 * g), dq = *(const f32x4*)(Dd + qs * 16 + 4 * g);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ql = qs * 16 + 4 * g + i;
-        float pv = fexp2(__builtin_fmaf(s[i], c, -Ls[ql]));
+        float pv = fexp2(__builtin_fmaf(s[i], c, -lq[i]));
         if (MODE == 0 && qt == kt && wave * 16 + li > ql) pv = 0.f;
         p[qs][i] = pv;
-        ds[qs][i] = pv * (dp[i] - Dd[ql]);
+        ds[qs][i] = pv * (dp[i] - dq[i]);
       }
     }
 #pragma unroll
