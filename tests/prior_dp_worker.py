@@ -21,21 +21,47 @@ def cfg():
     return P.PriorConfig(bins=64, ctx=256, width=128, depth=3, heads=2, blocks=4, attn_stacks=1)
 
 
-def build(process_group=None):
+def build(process_group=None, cond=False):
+    """cond: the upsampler form — level 0 of 2 with ConditionerNet on the level above (Sampler.py:24) and genre
+    labels (LabelConditioner), every parameter from the seeded store initialisation."""
     from oracle import prior_ref as P
     from prior import Prior
     c = cfg()
-    pr = Prior(0, [(c.ctx,)], c.bins, [3], [2], None,
-               dict(width=c.width, depth=c.depth, heads=c.heads, blocks=c.blocks, attn_stacks=c.attn_stacks,
-                    drop_out_rate=0.0), None, dtype="fp32", device="cuda:0", seed=3, process_group=process_group)
+    pk = dict(width=c.width, depth=c.depth, heads=c.heads, blocks=c.blocks, attn_stacks=c.attn_stacks,
+              drop_out_rate=0.0)
+    if cond:
+        ck = dict(dilation_factor=3, dilation_cycle=4, residual_width=32, residual_depth=8)
+        return Prior(0, [(c.ctx,), (c.ctx // 4,)], c.bins, [3, 2], [2, 2], None, pk, ck, genre_classes=10,
+                     dtype="fp32", device="cuda:0", seed=3, process_group=process_group)
+    pr = Prior(0, [(c.ctx,)], c.bins, [3], [2], None, pk, None, dtype="fp32", device="cuda:0", seed=3,
+               process_group=process_group)
     pr.prior.store.set_values(P.init_params(c, 3))
     return pr
 
 
-def batches(world):
+def batches(world, cond=False):
     c = cfg()
     g = torch.Generator().manual_seed(17)
-    return [torch.randint(0, c.bins - 1, (N_LOCAL * world, c.ctx), generator=g) for _ in range(2)]
+    out = []
+    for _ in range(2):
+        codes = torch.randint(0, c.bins - 1, (N_LOCAL * world, c.ctx), generator=g)
+        if cond:
+            out.append((codes, torch.randint(0, c.bins - 1, (N_LOCAL * world, c.ctx // 4), generator=g),
+                        torch.randint(0, 10, (N_LOCAL * world,), generator=g)))
+        else:
+            out.append(codes)
+    return out
+
+
+def shard(x, rank):
+    """rows [rank * N_LOCAL, +N_LOCAL) of a batch (a tensor or a tuple of tensors), on the device"""
+    if isinstance(x, tuple):
+        return tuple(t[rank * N_LOCAL:(rank + 1) * N_LOCAL].cuda() for t in x)
+    return x[rank * N_LOCAL:(rank + 1) * N_LOCAL].cuda()
+
+
+def to_dev(x):
+    return tuple(t.cuda() for t in x) if isinstance(x, tuple) else x.cuda()
 
 
 def snapshot(pr):
@@ -50,8 +76,10 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    pr = build()
-    xs = [x[rank * N_LOCAL:(rank + 1) * N_LOCAL].cuda() for x in batches(world)]
+    cond = mode.endswith("_cond")
+    mode = mode.replace("_cond", "")
+    pr = build(dist.group.WORLD, cond)
+    xs = [shard(x, rank) for x in batches(world, cond)]
     if mode == "eager":
         pr.train_step(xs[0])
         pr.train_step(xs[1])

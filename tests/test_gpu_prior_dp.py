@@ -33,7 +33,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph"])
+@pytest.mark.parametrize("mode", ["eager", "graph", "eager_cond", "graph_cond"])
 def test_prior_dp2_matches_single_process(cuda, tmp_path, mode):
     port = _port()
     procs, outs = [], []
@@ -46,8 +46,9 @@ def test_prior_dp2_matches_single_process(cuda, tmp_path, mode):
     for p in procs:
         assert p.wait(timeout=300) == 0
     r0, r1 = (torch.load(o, weights_only=True) for o in outs)
-    single = W.build()
-    xs = [x.cuda() for x in W.batches(2)]
+    cond = mode.endswith("_cond")  # the upsampler form: ConditionerNet on upper-level codes + genre labels
+    single = W.build(cond=cond)
+    xs = [W.to_dev(x) for x in W.batches(2, cond)]
     single.train_step(xs[0])
     single.train_step(xs[1])
     torch.cuda.synchronize()
