@@ -557,3 +557,25 @@ def test_decode_full_context_teacher_forced(cuda):
     torch.cuda.synchronize()
     ref = P.model_forward(p, full, tok[:, :L], x_cond=xc.double())
     assert _rel(dl, ref) < 2e-5
+
+
+def test_random_sample_search_matches_oracle_scores(cuda):
+    """autoregressive_fmha.py:242-302 random search: the product's per-sequence losses equal the fp64 oracle's
+    mean cross entropy of the same samples (1e-5), and the returned sample is the lowest-loss one of all rounds
+    among those passing the token-frequency rule (recomputed on the host from the same seeded samples)."""
+    m, p = _model(CFG)
+    L, iters, bpi, freq, seed = 60, 3, 4, 0.5, 11
+    best, best_loss = m.random_sample(seq_length=L, iterations=iters, batch_per_iter=bpi, token_freq=freq, seed=seed)
+    cands = []
+    for i in range(iters):
+        out = m.sample(bpi, max_length=L, seed=seed + i).cpu()
+        got = m.sequence_loss(out[:, :-1], out[:, 1:]).cpu().double()
+        logits = P.model_forward(p, CFG, out[:, :-1])
+        ref = (torch.logsumexp(logits, -1) - torch.gather(logits, -1, out[:, 1:, None]).squeeze(-1)).mean(dim=1)
+        assert _rel(got, ref) < 1e-5
+        for k in range(bpi):
+            _, counts = torch.unique(out[k], return_counts=True)
+            if int(counts.max()) < int(L * freq):
+                cands.append((float(got[k]), out[k]))
+    want = min(cands, key=lambda c: c[0])
+    assert abs(best_loss - want[0]) < 1e-6 and torch.equal(best.cpu(), want[1])

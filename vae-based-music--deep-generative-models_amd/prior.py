@@ -422,6 +422,58 @@ class FMHABasedAutoregressiveModel:
             return tokens, {}  # the decode kernel keeps no attention-weight tensors
         return tokens
 
+    def sequence_loss(self, inputs, targets, x_cond=None, y_cond=None, loss_fn=None):
+        """(N,) mean per-token cross entropy of `targets` under the model fed `inputs` (autoregressive.py:189-201
+        per sequence). loss_fn: None for the fused head (logits never written), or a callable on
+        (targets, (N, T, bins) logits) -> (N, T) losses (the logits are then materialised)."""
+        inputs = torch.as_tensor(inputs, device=self.device).long().contiguous()
+        targets = torch.as_tensor(targets, device=self.device).long().contiguous()
+        N, T = inputs.shape
+        if loss_fn is not None:
+            logits, _ = self(inputs, x_cond=x_cond, y_cond=y_cond)
+            return torch.as_tensor(loss_fn(targets, logits), device=self.device).float().reshape(N, T).mean(dim=1)
+        # every factorization is causal in time, so a partial last block is padded to the block length (the
+        # padded positions do not reach the first T) — the attention kernels take whole blocks
+        l = self.context_length // self.blocks
+        Tp = -(-T // l) * l
+        if Tp != T:
+            inputs = torch.nn.functional.pad(inputs, (0, Tp - T))
+            targets = torch.nn.functional.pad(targets, (0, Tp - T))
+        xc = self._cond(x_cond)
+        if xc is not None and xc.shape[1] > Tp:
+            xc = xc[:, :Tp].contiguous()
+        with torch.no_grad():
+            h = self.hidden(inputs, False, xc, self._ycond(y_cond))
+            lse = torch.empty(N * Tp, dtype=torch.float32, device=self.device)
+            loss_row = torch.empty_like(lse)
+            V.head_fwd(h, self._wt(self.cdt), self.store.view(self.out_bias), lse, targets=targets, loss_row=loss_row)
+        return loss_row.reshape(N, Tp)[:, :T].mean(dim=1)
+
+    def random_sample(self, loss_fn=None, seq_length=None, iterations=10, batch_per_iter=4, token_freq=0.50, seed=0):
+        """autoregressive_fmha.py:242-302 random search: `iterations` rounds of `batch_per_iter` ancestral samples
+        (round i draws its Gumbel noise with seed + i); each sample is scored by its own mean token loss under the
+        model, and a round's samples are taken in ascending loss while they beat the best so far — skipping any
+        in which one token fills >= int(seq_length * token_freq) of the (start-token-led) sequence. Returns (best
+        (seq_length + 1,) int64 sample with its start token — zeros (1, seq_length) if none qualified — , best
+        loss)."""
+        L = self.context_length if seq_length is None else int(seq_length)
+        best_loss = 1e10
+        best = torch.zeros(1, L, dtype=torch.int64, device=self.device)
+        limit = int(L * token_freq)
+        for i in range(iterations):
+            out = self.sample(batch_per_iter, max_length=L, seed=seed + i)  # (N, L + 1), start token first
+            loss = self.sequence_loss(out[:, :-1], out[:, 1:], loss_fn=loss_fn).cpu()
+            for k in torch.argsort(loss, stable=True).tolist():
+                cur = float(loss[k])
+                if not cur < best_loss:
+                    break
+                cand = out[k]
+                _, counts = torch.unique(cand, return_counts=True)
+                if int(counts.max()) >= limit:
+                    continue  # the reference prints "Token ... occurred ... Times! Skipping..."
+                best_loss, best = cur, cand
+        return best, best_loss
+
     @property
     def trainable_variables(self):
         return [self.store.view(n) for n, _, _ in self.store.specs if n.startswith(self.prefix + "/")]
