@@ -606,3 +606,29 @@ def test_get_vqvae_single_level_model(cuda):
     assert len(model.losses) == 1 and float(model.losses[0]) > 0
     with pytest.raises(ValueError):
         model(R.synthetic_batch(2, 1024, seed=8))
+
+
+def test_update_metrics_and_multispectral_loss_api(cuda):
+    """vqvae.py:262-304 update_metrics on given per-level losses (trackers = running means of the sums / the
+    per-level values, the reference's key set) and vqvae.py:309-326 _multispectral_loss (the product's
+    spectral-loss kernel through the reference's method name) vs the oracle's loss on the same reconstruction."""
+    from oracle import vqvae_ref as R
+    from vqvae import VQVAE
+    m = VQVAE((4096, 1), 2, 64, [3, 2], [2, 2], num_embeddings=64, residual_width=32, residual_depth=2,
+              dilation_factor=3, dtype="fp32", device="cuda")
+    for t in m.metrics:
+        t.reset_state()
+    out1 = m.update_metrics([1.0, 2.0], [0.5, 0.25], [0.125, 0.0625], [0.375, 1.6875])
+    out2 = m.update_metrics([3.0, 4.0], [0.5, 0.75], [0.125, 0.1875], [2.375, 3.0625])
+    assert float(out2["loss"]) == 5.0 and float(out2["recon_loss"]) == 1.0
+    assert abs(float(out2["vqvae_loss"]) - 0.25) < 1e-7 and abs(float(out2["spectral_loss"]) - 3.75) < 1e-6
+    assert float(m.level_loss_trackers[1].result()) == 3.0 and float(m.recon_loss_trackers[0].result()) == 0.5
+    per_level = {t.name for ts in (m.level_loss_trackers, m.recon_loss_trackers, m.vq_loss_trackers,
+                                   m.spectral_loss_trackers) for t in ts}
+    vq_names = {t.name for vq in m.vqs for t in vq.metrics}
+    assert set(out1) == {"loss", "recon_loss", "vqvae_loss", "spectral_loss"} | per_level | vq_names
+    x = R.synthetic_batch(2, 4096, seed=5)
+    r = x + 0.05 * np.random.default_rng(1).standard_normal(x.shape).astype(np.float32)
+    got = float(m._multispectral_loss(torch.from_numpy(x).cuda(), torch.from_numpy(r).cuda()))
+    ref = float(R.multispectral_loss(torch.from_numpy(x).double(), torch.from_numpy(r).double()).mean())
+    assert abs(got - ref) <= 1e-5 * abs(ref)

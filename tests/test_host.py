@@ -110,3 +110,25 @@ def test_keras_mean_trackers_monitor_loop():
     m.update_state(torch.tensor(5.0))
     m.reset_states()
     assert float(m.result()) == 0.0 and m.name == "x"
+
+
+def test_splitsongs_and_tile():
+    """data_utils.py:65-91 splitsongs (hand-derived: T=100, window 0.2 -> chunk 20, overlap 0.5 -> hop 10, starts
+    0..80 -> 9 chunks) and VectorQuantizer._tile (:191-199: ceil(K/N) repeats when N < K)."""
+    import numpy as np
+    import torch
+    from data_utils import splitsongs
+    from VectorQuantizer import VectorQuantizer
+    x = np.arange(100, dtype=np.float32)
+    xs, ys = splitsongs(x, 3, window=0.2, overlap=0.5)
+    assert xs.shape == (9, 20) and ys.tolist() == [3] * 9
+    assert xs[1, 0] == 10 and xs[-1, -1] == 99
+    xs2, _ = splitsongs(np.stack([x, -x]), 1, window=0.2, overlap=0.5)
+    assert xs2.shape == (9, 2, 20) and xs2[2, 1, 0] == -20
+    xs3, _ = splitsongs(np.arange(95, dtype=np.float32), 0, window=0.2, overlap=0.0)  # chunk 19, hop 19: 5 chunks
+    assert xs3.shape == (5, 19)
+    from types import SimpleNamespace
+    vq = SimpleNamespace(num_embeddings=8)  # _tile reads only K (the real layer allocates device state)
+    t = VectorQuantizer._tile(vq, torch.arange(12.).reshape(3, 4))
+    assert t.shape == (9, 4) and torch.equal(t[3:6], t[:3])
+    assert VectorQuantizer._tile(vq, torch.zeros(10, 4)).shape == (10, 4)

@@ -105,6 +105,16 @@ class VectorQuantizer:
         self._argmin(flat, idx)
         return idx
 
+    def _tile(self, x):
+        """VectorQuantizer.py:191-199: rows repeated ceil(K / N) times when N < K (so K candidate rows exist for
+        the dead-code reset). The product's reset draws the same rows by index (vqa_reset_perm_index takes the
+        row modulo N) without forming this tensor; this is the host-side form of the reference helper."""
+        x = torch.as_tensor(x)
+        nt, k = x.shape[0], self.num_embeddings
+        if nt < k:
+            return x.repeat((k + nt - 1) // nt, *([1] * (x.dim() - 1)))
+        return x
+
     def get_usage_count(self):
         return self.N_t
 

@@ -76,6 +76,21 @@ def multispectral_loss_and_grad(target: SpectralTarget, recon: torch.Tensor, los
     return loss, (dr.reshape(recon.shape) if need_grad else None)
 
 
+def splitsongs(X, y, window=0.05, overlap=0.5):
+    """data_utils.py:65-91: a song cut into overlapping chunks of int(T * window) samples, hopping by
+    int(chunk * (1 - overlap)); a chunk that would run past the end is dropped. X is (T,) or (C, T); returns
+    ((n, chunk) or (n, C, chunk), (n,) copies of the label) — channels first, as the reference's callers then
+    transpose to (B, T, C). Host numpy, like the reference (the training feed itself is generated on the
+    device: synthetic_batch_device)."""
+    X = np.asarray(X)
+    T = X.shape[-1]
+    chunk = int(T * window)
+    hop = int(chunk * (1.0 - overlap))
+    pieces = [X[..., s:s + chunk] for s in range(0, T - chunk + hop, hop)]
+    pieces = [p for p in pieces if p.shape[-1] == chunk]
+    return np.array(pieces), np.array([y] * len(pieces))
+
+
 def synthetic_batch(B: int, T: int, sr: int = 44100, seed: int = 1234) -> np.ndarray:
     """clip(0.5 sin(2 pi f t / sr + phi) + 0.05 N(0,1), -1, 1), f ~ U[55, 2000] Hz,
     phi ~ U[0, 2 pi). Shape (B, T, 1) fp32, never silent (the spectral loss has no epsilon)."""

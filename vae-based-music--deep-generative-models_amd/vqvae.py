@@ -282,6 +282,36 @@ class VQVAE:
         gradients (test_step) only the statistics region."""
         vqa_dp.exchange(self.bucket if grads else self._stats_region, self.process_group)
 
+    def update_metrics(self, level_losses, recon_losses, commit_losses, spectral_losses):
+        """vqvae.py:262-304 for externally computed per-level losses (the step itself updates the same
+        trackers in one launch, vqa_step_metrics): the total / recon / vq / spectral trackers take the sums over
+        levels, each level's trackers its own values; returns the reference's dict (the four totals, then per
+        level its trackers and its VectorQuantizer's)."""
+        def val(v):
+            return torch.as_tensor(v, dtype=torch.float32, device=self.device).reshape(())
+        lv, rv, cv, sv = ([val(v) for v in vs] for vs in (level_losses, recon_losses, commit_losses, spectral_losses))
+        self.total_loss_tracker.update_state(sum(lv))
+        self.reconstruction_loss_tracker.update_state(sum(rv))
+        self.vq_loss_tracker.update_state(sum(cv))
+        self.spectral_loss_tracker.update_state(sum(sv))
+        out = {"loss": self.total_loss_tracker.result(), "recon_loss": self.reconstruction_loss_tracker.result(),
+               "vqvae_loss": self.vq_loss_tracker.result(), "spectral_loss": self.spectral_loss_tracker.result()}
+        for l in range(self.levels):
+            for trackers, v in ((self.level_loss_trackers, lv), (self.recon_loss_trackers, rv),
+                                (self.vq_loss_trackers, cv), (self.spectral_loss_trackers, sv)):
+                trackers[l].update_state(v[l])
+                out[trackers[l].name] = trackers[l].result()
+            out.update({m.name: m.result() for m in self.vqs[l].metrics})
+        return out
+
+    def _multispectral_loss(self, x, reconstructions):
+        """vqvae.py:309-326: the multi-resolution spectral loss of `reconstructions` against `x` — the batch mean,
+        as a 0-dim device tensor (the reference's callers take tf.reduce_mean of it, which leaves it unchanged)."""
+        x = self._as_input(x)
+        r = torch.as_tensor(reconstructions, device=self.device).float().reshape(x.shape).contiguous()
+        loss, _ = multispectral_loss_and_grad(SpectralTarget(x), r, need_grad=False)
+        return loss.reshape(())
+
     def results(self) -> Dict[str, torch.Tensor]:
         res = self._macc[:, 0] / self._macc[:, 1].clamp(min=1.0)
         return {n: res[i] for i, n in enumerate(self.metric_names)}
