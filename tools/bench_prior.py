@@ -147,6 +147,28 @@ def main():
                           "config": {"workload": "BASELINE config 5", "ctx": a.ctx, "bins": a.bins, **kw},
                           "tokens_in_range": bool(((out_tok >= 0) & (out_tok < a.bins)).all())}), flush=True)
 
+    if a.only in ("", "sampler"):
+        # Sampler.py end to end: three levels top-down (n_ctxs of Sampler.py:127, the SMALL_* prior / conditioner
+        # settings of :24-25), each window one persistent decode launch, the lower ones conditioned on the codes
+        # drawn above them through ConditionerNet
+        from sampler import VQVAESampler
+        n_ctxs = [8192, 8192, 6144]
+        s = VQVAESampler([3, 2, 2], [2, 2, 2], n_ctxs, codebook_size=a.bins, dtype="fp32", device="cuda")
+        VQVAESampler([3, 2, 2], [2, 2, 2], [64, 16, 4], codebook_size=a.bins, priors=None, dtype="fp32",
+                     device="cuda").sample(a.samples, seed=1)  # warm-up (every kernel, conditioner included)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        zs = s.sample(a.samples, seed=2)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ntok = a.samples * sum(n_ctxs)
+        print(json.dumps({"metric": "tokens/sec VQVAESampler 3-level ancestral sampling (Sampler.py)",
+                          "value": round(ntok / el, 1), "unit": "tokens/s", "n_gpus": 1, "seconds": round(el, 3),
+                          "samples": a.samples, "n_ctxs": n_ctxs, "dtype": "fp32 (decode)",
+                          "config": {"workload": "BASELINE config 5 (Sampler.py)", "bins": a.bins, **kw},
+                          "shapes": [list(z.shape) for z in zs],
+                          "tokens_in_range": bool(all(((z >= 0) & (z < a.bins)).all() for z in zs))}), flush=True)
+
 
 if __name__ == "__main__":
     main()
