@@ -11,6 +11,11 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_prior.py tests/test_gpu_sam
 rc=$?
 tail -3 gpurun_out/variant_tests.log
 if [ $rc -ne 0 ]; then cp gpurun_out/base.so $L; echo "tests failed ($rc)"; exit $rc; fi
+for v in gpurun_out/base.so "$V"; do
+  cp "$v" $L
+  echo "== seqlin shapes: $(basename $v)"
+  timeout -k 10 120 python tools/seqlin_time.py || { cp gpurun_out/base.so $L; echo "seqlin_time failed"; exit 1; }
+done
 for r in 1 2; do
   for v in gpurun_out/base.so "$V"; do
     cp "$v" $L

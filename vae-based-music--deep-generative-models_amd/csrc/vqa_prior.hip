@@ -183,29 +183,58 @@ template <> struct RawR4<float> {
 // of every tap staged ONCE per workgroup in LDS; each wave takes 16 rows of a 64-row tile and loads its B
 // fragments (X^T: lane (row, g) <- 8 consecutive channels of its row) straight from global memory into
 // registers — no LDS copy of X, no barrier per tile — with the NEXT tile's fragments and residual rows
-// loaded while the current tile's MFMAs and stores run.
-constexpr int kSdRows = 64;
+// loaded while the current tile's MFMAs and stores run. The 1-tap epilogue goes through a per-wave fp32 LDS tile
+// (16 rows x N) so that bias, residual and the store run on row-contiguous 16-byte chunks (whole rows per
+// store instruction) instead of 4-channel pieces of 16 rows.
+constexpr int kSdRows = 64, kSdEpad = 4;
+
+// 16 bytes of activations <-> VEC / 4 groups of 4 fp32
+template <class T> __device__ __forceinline__ void chunk_widen(const uint4& u, f32x4* v) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 b = __builtin_bit_cast(bf16x8, u);
+    v[0] = f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+    v[1] = f32x4{(float)b[4], (float)b[5], (float)b[6], (float)b[7]};
+  } else {
+    v[0] = __builtin_bit_cast(f32x4, u);
+  }
+}
+template <class T> __device__ __forceinline__ uint4 chunk_narrow(const f32x4* v) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 b = {(bf16)v[0][0], (bf16)v[0][1], (bf16)v[0][2], (bf16)v[0][3],
+                      (bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]};
+    return __builtin_bit_cast(uint4, b);
+  } else {
+    return __builtin_bit_cast(uint4, v[0]);
+  }
+}
 
 template <class T, int K, int TAPS, int NT>
 __global__ __launch_bounds__(256) void seqlin_d_kernel(SeqLinArgs a, int ntiles) {
   typedef Mfma<T> M;
   typedef typename M::frag F;
   constexpr int PAD = 16 / (int)sizeof(T), VEC = 16 / (int)sizeof(T), KS = K + PAD, NKC = K / M::KS;
+  constexpr int NG = VEC / 4, IT = 16 * 16 * NT / VEC / 64;  // fp32 groups per chunk, chunks per lane (max)
+  // the LDS epilogue only where its tile keeps two workgroups per CU (the 3-tap images take ~80 KB already)
+  constexpr bool LE = TAPS == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Wt = (T*)smem;  // [TAPS * N][K + PAD]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, kof = M::koff(lane),
             g4 = 4 * (lane >> 4);
+  const int ES = a.N + kSdEpad, cpr = a.N / VEC, nch = 16 * cpr;
+  float* E = (float*)(Wt + TAPS * a.N * KS) + wave * 16 * ES;  // this wave's [16][N + pad] fp32 tile (LE)
   constexpr int CPR = K / VEC;
   for (int e = threadIdx.x; e < TAPS * a.N * CPR; e += 256) {
     const int n = e / CPR, q = e % CPR;
     *(uint4*)(Wt + n * KS + q * VEC) = *(const uint4*)((const T*)a.wp + (size_t)n * K + q * VEC);
   }
   F bf[2][TAPS][NKC];
-  RawR4<T> rr[2][NT];  // residual chunks (4 channels) of the lane's row per output tile
+  uint4 rr[2][IT];      // LE: residual chunks of the lane's output chunks
+  RawR4<T> r4[2][NT];   // otherwise: residual channels (4) of the lane's row per output tile
   // register double buffer: the slot is a compile-time constant (runtime-indexed register arrays spill)
   auto load_tile = [&](int tile, auto S) {
     constexpr int slot = decltype(S)::value;
-    const int seq = tile / a.tiles_per_seq, t = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16 + col;
+    const int seq = tile / a.tiles_per_seq, tb = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16,
+              t = tb + col;
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
       const int src = t + a.dir * (TAPS - 1 - tap);
@@ -219,11 +248,20 @@ __global__ __launch_bounds__(256) void seqlin_d_kernel(SeqLinArgs a, int ntiles)
       }
     }
     if (a.r) {
-      const bool ok = t < a.T;
-      const T* rp = (const T*)a.r + ((long long)seq * a.T + (ok ? t : 0)) * a.ldr + g4;
+      if constexpr (LE) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        if (nt * 16 < a.N) rr[slot][nt].v = *(const typename RawR4<T>::type*)(rp + nt * 16);
+        for (int i = 0; i < IT; ++i) {
+          const int e = lane + 64 * i, row = e / cpr, q = e - row * cpr;
+          if (e < nch && tb + row < a.T)
+            rr[slot][i] = *(const uint4*)((const T*)a.r + ((long long)seq * a.T + tb + row) * a.ldr + q * VEC);
+        }
+      } else {
+        const bool ok = t < a.T;
+        const T* rp = (const T*)a.r + ((long long)seq * a.T + (ok ? t : 0)) * a.ldr + g4;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          if (nt * 16 < a.N) r4[slot][nt].v = *(const typename RawR4<T>::type*)(rp + nt * 16);
+      }
     }
   };
   auto compute = [&](int tile, auto S) {
@@ -243,21 +281,61 @@ __global__ __launch_bounds__(256) void seqlin_d_kernel(SeqLinArgs a, int ntiles)
           acc[nt] = M::mma(M::load(wb + nt * 16 * KS), b, acc[nt]);
         }
       }
-    const int seq = tile / a.tiles_per_seq, t = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16 + col;
-    if (t < a.T) {
-      const long long row = (long long)seq * a.T + t;
+    if constexpr (!LE) {  // lane (row = col, g): channels nt*16 + 4g .. +3 of its row straight to memory
+      const int seq = tile / a.tiles_per_seq, t = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16 + col;
+      if (t < a.T) {
+        const long long row = (long long)seq * a.T + t;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        if (nt * 16 >= a.N) break;
-        const int c = nt * 16 + g4;
-        f32x4 v = acc[nt];
-        if (a.b) v = v + f32x4{a.b[c], a.b[c + 1], a.b[c + 2], a.b[c + 3]};
-        if (a.r) v = v + rr[slot][nt].f();
-        T* yp = (T*)a.y + row * a.ldy + c;
-        if (a.accumulate) v = v + ld4((const T*)yp);
-        st4(yp, v);
+        for (int nt = 0; nt < NT; ++nt) {
+          if (nt * 16 >= a.N) break;
+          const int c = nt * 16 + g4;
+          f32x4 v = acc[nt];
+          if (a.b) v = v + f32x4{a.b[c], a.b[c + 1], a.b[c + 2], a.b[c + 3]};
+          if (a.r) v = v + r4[slot][nt].f();
+          T* yp = (T*)a.y + row * a.ldy + c;
+          if (a.accumulate) v = v + ld4((const T*)yp);
+          st4(yp, v);
+        }
       }
+      return;
     }
+    // lane (row = col, g) holds channels nt*16 + 4g .. +3 -> the wave's fp32 tile; LDS traffic of one wave
+    // is processed in order, so its reads below see these writes
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      if (nt * 16 >= a.N) break;
+      *(f32x4*)(E + col * ES + nt * 16 + g4) = acc[nt];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int seq = tile / a.tiles_per_seq, tb = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = lane + 64 * i, row = e / cpr, q = e - row * cpr;
+      if (e >= nch || tb + row >= a.T) continue;
+      const long long grow = (long long)seq * a.T + tb + row;
+      f32x4 v[NG], u[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) v[g] = *(const f32x4*)(E + row * ES + q * VEC + 4 * g);
+      if (a.b)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const float* bp = a.b + q * VEC + 4 * g;  // parameter views need not be 16-byte aligned
+          v[g] = v[g] + f32x4{bp[0], bp[1], bp[2], bp[3]};
+        }
+      if (a.r) {
+        chunk_widen<T>(rr[slot][i], u);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) v[g] = v[g] + u[g];
+      }
+      uint4* yp = (uint4*)((T*)a.y + grow * a.ldy + q * VEC);
+      if (a.accumulate) {
+        chunk_widen<T>(*yp, u);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) v[g] = v[g] + u[g];
+      }
+      *yp = chunk_narrow<T>(v);
+    }
+    __builtin_amdgcn_wave_barrier();
   };
   typedef std::integral_constant<int, 0> S0;
   typedef std::integral_constant<int, 1> S1;
@@ -1666,7 +1744,8 @@ template <class T>
 static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
   if (a.wp) {
     const int KS = a.K + 16 / (int)sizeof(T);
-    const size_t lds = (size_t)a.taps * a.N * KS * sizeof(T);
+    const size_t lds = (size_t)a.taps * a.N * KS * sizeof(T) +
+                       (a.taps == 1 ? (size_t)4 * 16 * (a.N + kSdEpad) * sizeof(float) : 0);
     const void* fn = nullptr;
     const bool n2 = a.N <= 32;
 #define VQA_SD(KK, TT)                                                                                  \
@@ -1674,7 +1753,11 @@ static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
       fn = n2 ? (const void*)seqlin_d_kernel<T, KK, TT, 2> : (const void*)seqlin_d_kernel<T, KK, TT, 8>;
     VQA_SD(32, 1) VQA_SD(128, 1) VQA_SD(96, 3) VQA_SD(128, 3)
 #undef VQA_SD
-    if (fn && lds <= 160 * 1024) {
+    // the 1-tap epilogue stores (and reads the residual) in whole 16-byte chunks
+    const int vec = 16 / (int)sizeof(T);
+    const bool chunks = a.taps != 1 || (a.ldy % vec == 0 && ((uintptr_t)a.y & 15) == 0 &&
+                                        (!a.r || (a.ldr % vec == 0 && ((uintptr_t)a.r & 15) == 0)));
+    if (fn && chunks && lds <= 160 * 1024) {
       if (int rc = set_lds_attr(fn, lds)) return rc;
       SeqLinArgs c = a;
       c.tiles_per_seq = (a.T + kSdRows - 1) / kSdRows;
