@@ -186,7 +186,7 @@ template <> struct RawR4<float> {
 // loaded while the current tile's MFMAs and stores run. The 1-tap epilogue goes through a per-wave fp32 LDS tile
 // (16 rows x N) so that bias, residual and the store run on row-contiguous 16-byte chunks (whole rows per
 // store instruction) instead of 4-channel pieces of 16 rows.
-constexpr int kSdRows = 64, kSdEpad = 4;
+constexpr int kSdEpad = 4;
 
 // 16 bytes of activations <-> VEC / 4 groups of 4 fp32
 template <class T> __device__ __forceinline__ void chunk_widen(const uint4& u, f32x4* v) {
@@ -208,8 +208,8 @@ template <class T> __device__ __forceinline__ uint4 chunk_narrow(const f32x4* v)
   }
 }
 
-template <class T, int K, int TAPS, int NT>
-__global__ __launch_bounds__(256) void seqlin_d_kernel(SeqLinArgs a, int ntiles) {
+template <class T, int K, int TAPS, int NT, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int ntiles) {
   typedef Mfma<T> M;
   typedef typename M::frag F;
   constexpr int PAD = 16 / (int)sizeof(T), VEC = 16 / (int)sizeof(T), KS = K + PAD, NKC = K / M::KS;
@@ -223,10 +223,11 @@ __global__ __launch_bounds__(256) void seqlin_d_kernel(SeqLinArgs a, int ntiles)
   const int ES = a.N + kSdEpad, cpr = a.N / VEC, nch = 16 * cpr;
   float* E = (float*)(Wt + TAPS * a.N * KS) + wave * 16 * ES;  // this wave's [16][N + pad] fp32 tile (LE)
   constexpr int CPR = K / VEC;
-  for (int e = threadIdx.x; e < TAPS * a.N * CPR; e += 256) {
+  for (int e = threadIdx.x; e < TAPS * a.N * CPR; e += 64 * WAVES) {
     const int n = e / CPR, q = e % CPR;
     *(uint4*)(Wt + n * KS + q * VEC) = *(const uint4*)((const T*)a.wp + (size_t)n * K + q * VEC);
   }
+  constexpr int kSdRows = 16 * WAVES;
   F bf[2][TAPS][NKC];
   uint4 rr[2][IT];      // LE: residual chunks of the lane's output chunks
   RawR4<T> r4[2][NT];   // otherwise: residual channels (4) of the lane's row per output tile
@@ -1743,14 +1744,18 @@ static int set_lds_attr(const void* fn, size_t bytes) {
 template <class T>
 static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
   if (a.wp) {
+    // wide outputs: 8 waves per workgroup share one staged weight image (one workgroup per CU); narrow ones:
+    // 4 waves, two workgroups per CU (measured per shape, tools/seqlin_time.py)
+    const bool n2 = a.N <= 32, w8 = a.N >= 96;
+    const int waves = w8 ? 8 : 4, max_per_cu = w8 ? 1 : 2;
     const int KS = a.K + 16 / (int)sizeof(T);
     const size_t lds = (size_t)a.taps * a.N * KS * sizeof(T) +
-                       (a.taps == 1 ? (size_t)4 * 16 * (a.N + kSdEpad) * sizeof(float) : 0);
+                       (a.taps == 1 ? (size_t)waves * 16 * (a.N + kSdEpad) * sizeof(float) : 0);
     const void* fn = nullptr;
-    const bool n2 = a.N <= 32;
-#define VQA_SD(KK, TT)                                                                                  \
-    if (a.K == KK && a.taps == TT)                                                                    \
-      fn = n2 ? (const void*)seqlin_d_kernel<T, KK, TT, 2> : (const void*)seqlin_d_kernel<T, KK, TT, 8>;
+#define VQA_SD(KK, TT)                                                                                         \
+    if (a.K == KK && a.taps == TT)                                                                           \
+      fn = n2 ? (const void*)seqlin_d_kernel<T, KK, TT, 2, 4>                                                \
+              : w8 ? (const void*)seqlin_d_kernel<T, KK, TT, 8, 8> : (const void*)seqlin_d_kernel<T, KK, TT, 8, 4>;
     VQA_SD(32, 1) VQA_SD(128, 1) VQA_SD(96, 3) VQA_SD(128, 3)
 #undef VQA_SD
     // the 1-tap epilogue stores (and reads the residual) in whole 16-byte chunks
@@ -1760,12 +1765,12 @@ static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
     if (fn && chunks && lds <= 160 * 1024) {
       if (int rc = set_lds_attr(fn, lds)) return rc;
       SeqLinArgs c = a;
-      c.tiles_per_seq = (a.T + kSdRows - 1) / kSdRows;
+      c.tiles_per_seq = (a.T + 16 * waves - 1) / (16 * waves);
       int ntiles = a.nseq * c.tiles_per_seq;
-      const int per_cu = std::max(1, std::min<int>(2, (int)(160 * 1024 / lds)));
+      const int per_cu = std::max(1, std::min<int>(max_per_cu, (int)(160 * 1024 / lds)));
       const int nwg = std::min(ntiles, pr_cus() * per_cu);
       void* args[] = {&c, &ntiles};
-      (void)hipLaunchKernel(fn, dim3(nwg), dim3(256), args, lds, s);
+      (void)hipLaunchKernel(fn, dim3(nwg), dim3(64 * waves), args, lds, s);
       VQA_LAUNCHED("seqlin_d_kernel");
       return VQA_OK;
     }
