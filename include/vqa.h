@@ -298,6 +298,14 @@ int vqa_seqlin_prep(const vqa_seqlin_prep_desc* descs, int count, int dtype, vqa
 int vqa_seqlin_fwd_prepped(const void* x, int64_t ldx, const void* wp, const float* bias, const void* residual,
                            int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K, int N, int taps, int dir,
                            int accumulate, int dtype, vqa_stream_t stream);
+/* vqa_seqlin_fwd_prepped of LayerNorm(x; gamma, beta, eps) without materialising it: transformer.py:24-30's
+ * LayerNorm -> FactorizedAttention qkv Conv1D and LayerNorm -> mlp Dense (+ x1) in one launch. Bit-identical to
+ * vqa_layernorm_fwd followed by vqa_seqlin_fwd_prepped (rows outside [0, T) are zero, not beta). bf16, K = 128
+ * only; VQA_E_UNSUPPORTED otherwise (callers then run the two launches). */
+int vqa_seqlin_fwd_ln_prepped(const void* x, int64_t ldx, const float* gamma, const float* beta, float eps,
+                              const void* wp, const float* bias, const void* residual, int64_t ldr, void* y,
+                              int64_t ldy, int nseq, int T, int K, int N, int taps, int dir, int dtype,
+                              vqa_stream_t stream);
 /* dW[tap][k][n] = sum_t x[t-(taps-1-tap)][k] dy[t][n], db = sum_t dy[t] (deterministic partials; desc != NULL
  * defers the reduction as for the conv weight gradients). K <= 128, N <= 128, multiples of 16. */
 size_t vqa_seqlin_wgrad_workspace(int nseq, int T, int K, int N, int taps);

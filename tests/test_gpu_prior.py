@@ -85,6 +85,51 @@ def test_seqlin_column_slices(cuda):
     assert _rel(out[..., 64:96], ref) < 2e-6 and float(out[..., :64].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("K,N,taps,dir,T,res", [(128, 96, 3, -1, 200, False), (96, 128, 3, 1, 200, False),
+                                                (32, 32, 1, -1, 136, False), (32, 128, 1, -1, 130, True),
+                                                (128, 128, 1, -1, 130, True), (128, 32, 1, -1, 64, False)])
+def test_seqlin_prepped_and_fused_layernorm(cuda, K, N, taps, dir, T, res):
+    """Prepared-weight form (seqlin_d: 1-tap LDS epilogue, 8-wave launches for N >= 96) on ragged T vs fp64, and
+    the LayerNorm-fused form (vqa_seqlin_fwd_ln_prepped, K = 128) BIT-identical to layernorm_fwd + the prepped
+    launch; fp32 activations are refused by the fused form."""
+    import vqa_lib as V
+    dt, nseq = torch.bfloat16, 3
+    g = _gen(K * N + taps + T)
+    x = (torch.randn(nseq, T, K, generator=g) * 1.5 + 0.3).to(dt).cuda()
+    w = (torch.randn(taps, K, N, generator=g) / math.sqrt(K * taps)).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    r = torch.randn(nseq, T, N, generator=g).to(dt).cuda() if res else None
+    wp = torch.empty(taps, N, K, dtype=dt, device="cuda")
+    V.seqlin_prep([(w, wp, taps, K, N, False)], dt)
+    y = torch.empty(nseq, T, N, dtype=dt, device="cuda")
+    V.seqlin_fwd_prepped(x, wp, b, y, T, taps=taps, dir=dir, residual=r)
+    torch.cuda.synchronize()
+    xr, wr = x.double().cpu(), w.double().cpu()
+    if taps == 3:
+        # dir -1: rows t-2, t-1, t (causal conv); dir +1: rows t+2, t+1, t with the same tap weights
+        ref = P.causal_conv(xr, wr, b.double().cpu()) if dir == -1 else \
+            P.causal_conv(xr.flip(1), wr, b.double().cpu()).flip(1)
+    else:
+        ref = xr @ wr[0] + b.double().cpu()
+    if res:
+        ref = ref + r.double().cpu()
+    assert _rel(y, ref) < 2e-2
+    if K != 128:
+        return
+    gm = (1.0 + 0.2 * torch.randn(K, generator=g)).cuda()
+    bt = (0.1 * torch.randn(K, generator=g)).cuda()
+    a = torch.empty_like(x)
+    V.layernorm_fwd(x, gm, bt, a, 1e-6)
+    y0 = torch.empty_like(y)
+    V.seqlin_fwd_prepped(a, wp, b, y0, T, taps=taps, dir=dir, residual=r)
+    y1 = torch.full_like(y, float("nan"))
+    V.seqlin_fwd_ln_prepped(x, gm, bt, 1e-6, wp, b, y1, T, taps=taps, dir=dir, residual=r)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    with pytest.raises(Exception):
+        V.seqlin_fwd_ln_prepped(x.float(), gm, bt, 1e-6, wp, b, y1.float(), T, taps=taps, dir=dir)
+
+
 # ------------------------------------------------------------------ attention
 def _attn_ref(q, k, v, mode, l, H, vbias):
     """Core of keras MultiHeadAttention on projected heads (N, T, H*16), by the oracle's factorizations with

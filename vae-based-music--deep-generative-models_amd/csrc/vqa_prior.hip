@@ -69,6 +69,9 @@ struct SeqLinArgs {
   void* y;
   long long ldx, ldr, ldy;
   int nseq, T, K, N, taps, dir, wtrans, accumulate, tiles_per_seq;
+  const float* lng;  // optional (seqlin_d, bf16, K = 128): LayerNorm(gamma, beta, eps) of each input row first
+  const float* lnb;
+  float lneps;
 };
 
 constexpr int kSlRows = 128;
@@ -208,6 +211,44 @@ template <class T> __device__ __forceinline__ uint4 chunk_narrow(const f32x4* v)
   }
 }
 
+// LayerNorm of one row held as the B fragments of a 128-channel row (bf16, lane (row, g) holds channels
+// 32 kc + 8 g .. +7 in fragment kc): the same arithmetic as layernorm8_fwd_kernel<bf16, 16> (vqa_cond.hip) —
+// per-chunk sequential sums, then its butterfly over the 16 chunks (chunk bits 3, 2 are the fragment index
+// bits 1, 0 here; chunk bits 1, 0 are lane bits 5, 4) — so the fused and the unfused forms are bit-identical.
+__device__ __forceinline__ void ln_row_frags(bf16x8 (&x)[4], const float* gs, const float* bs, int g8, float eps) {
+  // the bf16 inputs are re-widened per pass (cheap) rather than held as 32 fp32 registers
+  auto bfly = [](const float (&c)[4]) {
+    float u = (c[0] + c[2]) + (c[1] + c[3]);
+    u += __shfl_xor(u, 32, 64);
+    u += __shfl_xor(u, 16, 64);
+    return u;
+  };
+  float s[4];
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    s[kc] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[kc] += (float)x[kc][i];
+  }
+  const float mean = bfly(s) / 128.f;
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    s[kc] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = (float)x[kc][i] - mean;
+      s[kc] += d * d;
+    }
+  }
+  const float inv = 1.0f / sqrtf(bfly(s) / 128.f + eps);
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      x[kc][i] = (bf16)(((float)x[kc][i] - mean) * inv * gs[32 * kc + g8 + i] + bs[32 * kc + g8 + i]);
+  }
+}
+
 template <class T, int K, int TAPS, int NT, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int ntiles) {
   typedef Mfma<T> M;
@@ -222,6 +263,12 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
             g4 = 4 * (lane >> 4);
   const int ES = a.N + kSdEpad, cpr = a.N / VEC, nch = 16 * cpr;
   float* E = (float*)(Wt + TAPS * a.N * KS) + wave * 16 * ES;  // this wave's [16][N + pad] fp32 tile (LE)
+  // LayerNorm parameters (LN form): after the image and the epilogue tiles
+  float* Lg = (float*)(Wt + TAPS * a.N * KS) + (LE ? WAVES * 16 * ES : 0);
+  constexpr bool LNF = sizeof(T) == 2 && K == 128;
+  if constexpr (LNF)
+    if (a.lng)
+      for (int e = threadIdx.x; e < 2 * K; e += 64 * WAVES) Lg[e] = e < K ? a.lng[e] : a.lnb[e - K];
   constexpr int CPR = K / VEC;
   for (int e = threadIdx.x; e < TAPS * a.N * CPR; e += 64 * WAVES) {
     const int n = e / CPR, q = e % CPR;
@@ -267,6 +314,20 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
   };
   auto compute = [&](int tile, auto S) {
     constexpr int slot = decltype(S)::value;
+    if constexpr (LNF) {
+      if (a.lng) {  // normalise the rows now (their loads have landed); rows outside [0, T) stay zero
+        const int seq = tile / a.tiles_per_seq, t = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16 + col;
+#pragma unroll
+        for (int tap = 0; tap < TAPS; ++tap) {
+          const int src = t + a.dir * (TAPS - 1 - tap);
+          ln_row_frags(bf[slot][tap], Lg, Lg + K, kof, a.lneps);
+          if (!(src >= 0 && src < a.T && t < a.T))
+#pragma unroll
+            for (int kc = 0; kc < NKC; ++kc) bf[slot][tap][kc] = F{};
+          __builtin_amdgcn_sched_barrier(0);  // one row set at a time (register pressure)
+        }
+      }
+    }
     f32x4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1750,7 +1811,8 @@ static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
     const int waves = w8 ? 8 : 4, max_per_cu = w8 ? 1 : 2;
     const int KS = a.K + 16 / (int)sizeof(T);
     const size_t lds = (size_t)a.taps * a.N * KS * sizeof(T) +
-                       (a.taps == 1 ? (size_t)waves * 16 * (a.N + kSdEpad) * sizeof(float) : 0);
+                       (a.taps == 1 ? (size_t)waves * 16 * (a.N + kSdEpad) * sizeof(float) : 0) +
+                       (a.lng ? (size_t)2 * a.K * sizeof(float) : 0);
     const void* fn = nullptr;
 #define VQA_SD(KK, TT)                                                                                         \
     if (a.K == KK && a.taps == TT)                                                                           \
@@ -1776,6 +1838,8 @@ static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
     }
     // weights too large for one LDS image: stage per tap from the prepared image
   }
+  VQA_REQUIRE(!a.lng, VQA_E_UNSUPPORTED, "seqlin_fwd_ln_prepped: K=%d N=%d taps=%d has no fused form", a.K, a.N,
+              a.taps);
   const void* fn = a.N <= 32 ? (const void*)seqlin_kernel<T, 2> : (const void*)seqlin_kernel<T, 8>;
   const size_t lds = seqlin_lds(a.K, a.N, a.taps, sizeof(T));
   if (int rc = set_lds_attr(fn, lds)) return rc;
@@ -1855,6 +1919,22 @@ extern "C" int vqa_seqlin_fwd_prepped(const void* x, int64_t ldx, const void* wp
   VQA_ARG(wp, "seqlin_fwd_prepped: no weights");
   return seqlin_launch(x, ldx, nullptr, wp, bias, residual, ldr, y, ldy, nseq, T, K, N, taps, dir, 0, accumulate,
                        dtype, (hipStream_t)stream);
+}
+
+extern "C" int vqa_seqlin_fwd_ln_prepped(const void* x, int64_t ldx, const float* gamma, const float* beta,
+                                         float eps, const void* wp, const float* bias, const void* residual,
+                                         int64_t ldr, void* y, int64_t ldy, int nseq, int T, int K, int N, int taps,
+                                         int dir, int dtype, vqa_stream_t stream) {
+  VQA_ARG(x && wp && y && gamma && beta && nseq > 0 && T > 0 && (taps == 1 || taps == 3) && (dir == -1 || dir == 1),
+          "seqlin_fwd_ln_prepped: bad arguments");
+  VQA_REQUIRE(dtype == VQA_BF16 && K == 128 && N > 0 && N <= 128 && N % 16 == 0, VQA_E_UNSUPPORTED,
+              "seqlin_fwd_ln_prepped: dtype %d K=%d N=%d unsupported (bf16, K = 128)", dtype, K, N);
+  VQA_ARG(ldx % 8 == 0 && ldx >= K && ldy >= N && ldy % 4 == 0 && (!residual || ldr % 4 == 0),
+          "seqlin_fwd_ln_prepped: strides must keep 16-byte rows");
+  VQA_ARG(((uintptr_t)wp & 15) == 0, "seqlin_fwd_ln_prepped: weights must be 16-byte aligned");
+  SeqLinArgs a{x, nullptr, wp, bias, residual, y, ldx, ldr, ldy, nseq, T, K, N, taps, dir, 0, 0,
+               (T + kSlRows - 1) / kSlRows, gamma, beta, eps};
+  return launch_seqlin<bf16>(a, (hipStream_t)stream);
 }
 
 extern "C" size_t vqa_seqlin_wgrad_workspace(int nseq, int T, int K, int N, int taps) {

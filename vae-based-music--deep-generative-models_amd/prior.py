@@ -134,13 +134,17 @@ class ResidualAttnBlock:
         """x (N, T, d) -> (N, T, d). save: keep what backward needs (layer input, qkv, heads, lse, o32, x1)."""
         f, cdt, eps = self.fmha, x.dtype, 1e-6
         N = x.shape[0]
-        a = torch.empty_like(x)
-        V.layernorm_fwd(x, self.store.view(f"{self.prefix}/ln1/gamma"), self.store.view(f"{self.prefix}/ln1/beta"), a,
-                        eps)
         w = f.width
         qkv = torch.empty(N, T, 3 * w, dtype=cdt, device=x.device)
         wp = self.wp
-        V.seqlin_fwd_prepped(a, wp["qkv"], f.p("qkv/bias"), qkv, T, taps=3, dir=-1)
+        g1, b1 = self.store.view(f"{self.prefix}/ln1/gamma"), self.store.view(f"{self.prefix}/ln1/beta")
+        fused = V.seqlin_fused_ln_ok(x, x.shape[-1])  # LayerNorm inside the consumer's row loads (bit-identical)
+        if fused:
+            V.seqlin_fwd_ln_prepped(x, g1, b1, eps, wp["qkv"], f.p("qkv/bias"), qkv, T, taps=3, dir=-1)
+        else:
+            a = torch.empty_like(x)
+            V.layernorm_fwd(x, g1, b1, a, eps)
+            V.seqlin_fwd_prepped(a, wp["qkv"], f.p("qkv/bias"), qkv, T, taps=3, dir=-1)
         heads = []
         for j, n in enumerate(("query", "key", "value")):
             h = torch.empty(N, T, w, dtype=cdt, device=x.device)
@@ -161,11 +165,15 @@ class ResidualAttnBlock:
             V.axpy(x1, x, x1)
         else:
             V.seqlin_fwd_prepped(o32, wp["proj"], f.p("proj/bias"), x1, T, residual=x)
-        h2 = torch.empty_like(x)
-        V.layernorm_fwd(x1, self.store.view(f"{self.prefix}/ln2/gamma"), self.store.view(f"{self.prefix}/ln2/beta"),
-                        h2, eps)
+        g2, b2 = self.store.view(f"{self.prefix}/ln2/gamma"), self.store.view(f"{self.prefix}/ln2/beta")
         out = torch.empty_like(x)
-        V.seqlin_fwd_prepped(h2, wp["mlp"], self.store.view(f"{self.prefix}/mlp/bias"), out, T, residual=x1)
+        if fused:
+            V.seqlin_fwd_ln_prepped(x1, g2, b2, eps, wp["mlp"], self.store.view(f"{self.prefix}/mlp/bias"), out, T,
+                                    residual=x1)
+        else:
+            h2 = torch.empty_like(x)
+            V.layernorm_fwd(x1, g2, b2, h2, eps)
+            V.seqlin_fwd_prepped(h2, wp["mlp"], self.store.view(f"{self.prefix}/mlp/bias"), out, T, residual=x1)
         self._saved = (x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter) if save else None
         return out
 

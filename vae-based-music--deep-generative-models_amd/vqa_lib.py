@@ -36,7 +36,7 @@ EXPORTED = [
     "vqa_step_metrics", "vqa_synthetic_batch",
     "vqa_embedding_fwd", "vqa_embedding_bwd", "vqa_embedding_bwd_workspace", "vqa_layernorm_fwd",
     "vqa_layernorm_bwd", "vqa_layernorm_bwd_workspace",
-    "vqa_seqlin_fwd", "vqa_seqlin_prep", "vqa_seqlin_fwd_prepped", "vqa_seqlin_wgrad_workspace", "vqa_seqlin_wgrad", "vqa_prior_embed_fwd", "vqa_colsum",
+    "vqa_seqlin_fwd", "vqa_seqlin_prep", "vqa_seqlin_fwd_prepped", "vqa_seqlin_fwd_ln_prepped", "vqa_seqlin_wgrad_workspace", "vqa_seqlin_wgrad", "vqa_prior_embed_fwd", "vqa_colsum",
     "vqa_axpy", "vqa_dropout", "vqa_scale_f32", "vqa_tf_mix", "vqa_attn_fwd", "vqa_attn_bwd", "vqa_head_wt",
     "vqa_head_fwd", "vqa_head_bwd_workspace", "vqa_head_bwd", "vqa_rowsum_workspace", "vqa_rowsum", "vqa_prior_decode_cache_bytes",
     "vqa_prior_decode",
@@ -117,6 +117,7 @@ _SIGS = {
     "vqa_seqlin_fwd": (_I, [_P, _L, _P, _P, _P, _L, _P, _L] + [_I] * 9 + [_P]),
     "vqa_seqlin_prep": (_I, [_P, _I, _I, _P]),
     "vqa_seqlin_fwd_prepped": (_I, [_P, _L, _P, _P, _P, _L, _P, _L] + [_I] * 8 + [_P]),
+    "vqa_seqlin_fwd_ln_prepped": (_I, [_P, _L, _P, _P, ctypes.c_float, _P, _P, _P, _L, _P, _L] + [_I] * 7 + [_P]),
     "vqa_seqlin_wgrad_workspace": (_S, [_I] * 5),
     "vqa_seqlin_wgrad": (_I, [_P, _L, _P, _L, _P, _P] + [_I] * 6 + [_P, _S, _P, _P]),
     "vqa_prior_embed_fwd": (_I, [_P] * 6 + [_I] * 4 + [_F, _F, _U, _P, _I, _P]),
@@ -580,6 +581,23 @@ def seqlin_fwd_prepped(x, wp, b, y, T, taps=1, dir=-1, residual=None, accumulate
     _check(lib().vqa_seqlin_fwd_prepped(px, ldx, ptr(wp), ptr(b), pr, ldr, py, ldy, rows // T, T, K, N, taps, dir,
                                         int(bool(accumulate)), dtype_code(x.dtype), stream()),
            "vqa_seqlin_fwd_prepped")
+
+
+def seqlin_fused_ln_ok(x, K):
+    """vqa_seqlin_fwd_ln_prepped's domain: bf16 activations with K = 128 channels."""
+    return x.dtype == torch.bfloat16 and K == 128
+
+
+def seqlin_fwd_ln_prepped(x, gamma, beta, eps, wp, b, y, T, taps=1, dir=-1, residual=None):
+    """vqa_seqlin_fwd_ln_prepped: seqlin_fwd_prepped(LayerNorm(x)) in one launch (bf16, K = 128)."""
+    px, ldx = rptr(x)
+    py, ldy = rptr(y)
+    pr, ldr = rptr(residual) if residual is not None else (None, 0)
+    K, N = x.shape[-1], y.shape[-1]
+    rows = x.numel() // K
+    _check(lib().vqa_seqlin_fwd_ln_prepped(px, ldx, ptr(gamma), ptr(beta), float(eps), ptr(wp), ptr(b), pr, ldr, py,
+                                           ldy, rows // T, T, K, N, taps, dir, dtype_code(x.dtype), stream()),
+           "vqa_seqlin_fwd_ln_prepped")
 
 
 def seqlin_wgrad(x, dy, dw, db, T, taps=1, deferred=None):
