@@ -100,7 +100,7 @@ def main():
         att_flop = a.batch * 2 * 4 * (a.ctx // 4) * (a.ctx // 4 + 64) / 2 * 16 * 2 * 2
         t_head = timed(lambda: V.head_fwd(x, wt, hb, hl, amax=am))
         head_flop = 2.0 * M * 128 * a.bins
-        out["roofline"] = {"kernel": "seqlin_kernel<bf16> (Dense 128->128 + residual, the mlp / proj form)",
+        out["roofline"] = {"kernel": "seqlin_d_kernel<bf16,128,1,8,8> (Dense 128->128 + residual, the mlp form, prepared weights)",
                            "bound": "hbm", "achieved": round(lin_bytes / t_lin / 1e3, 1), "peak": 8000.0,
                            "unit": "GB/s", "frac": round(lin_bytes / t_lin / 1e3 / 8000.0, 4),
                            "avg_launch_us": round(t_lin, 2), "algorithmic_bytes_per_launch": lin_bytes}
