@@ -3,7 +3,9 @@
 Runs VQVAE.train_step with a torch.distributed process group (gloo, every rank on cuda:0) on its shard of
 the global batch — eager, or as the two captured hipGraphs around the eager all_reduce — then one
 `vqvaes[0](x, training=True)` forward (the EMA on global statistics), and saves the resulting state.
-    python tests/dp_worker.py MODE OUT   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment)
+    python tests/dp_worker.py MODE OUT [CONFIG [DTYPE]]   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set)
+CONFIG "cfg1" is BASELINE config 1's architecture; "cfg2_short" is the benched architecture (config 2/3: 3
+levels, K = 2048, down_depth [3,2,2], concurrent level streams) on an 8192-frame chunk.
 """
 import os
 import sys
@@ -14,18 +16,23 @@ sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-CFG = dict(input_len=4096, levels=1, latent_dim=64, down_depth=[3], strides=[2], num_embeddings=256,
-           residual_width=32, residual_depth=4, dilation_factor=3)
+CONFIGS = {
+    "cfg1": dict(input_len=4096, levels=1, latent_dim=64, down_depth=[3], strides=[2], num_embeddings=256,
+                 residual_width=32, residual_depth=4, dilation_factor=3),
+    "cfg2_short": dict(input_len=8192, levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2],
+                       num_embeddings=2048, residual_width=32, residual_depth=4, dilation_factor=3),
+}
+CFG = CONFIGS["cfg1"]
 B_LOCAL = 2
 
 
-def build(B, process_group=None):
+def build(B, process_group=None, config="cfg1", dtype="fp32"):
     from oracle import vqvae_ref as R
     from vqvae import VQVAE
-    cfg = R.RefConfig(**CFG)
+    cfg = R.RefConfig(**CONFIGS[config])
     m = VQVAE((cfg.input_len, 1), cfg.levels, cfg.latent_dim, cfg.down_depth, cfg.strides,
               num_embeddings=cfg.num_embeddings, residual_width=cfg.residual_width,
-              residual_depth=cfg.residual_depth, dilation_factor=cfg.dilation_factor, dtype="fp32",
+              residual_depth=cfg.residual_depth, dilation_factor=cfg.dilation_factor, dtype=dtype,
               device="cuda:0", process_group=process_group)
     m.set_weights(R.init_params(cfg, 1))
     m.set_vq_state(R.init_vq_state(cfg, 2))
@@ -33,9 +40,9 @@ def build(B, process_group=None):
     return m
 
 
-def batches(world):
+def batches(world, config="cfg1"):
     from oracle import vqvae_ref as R
-    return [R.synthetic_batch(B_LOCAL * world, CFG["input_len"], seed=90 + i) for i in range(3)]
+    return [R.synthetic_batch(B_LOCAL * world, CONFIGS[config]["input_len"], seed=90 + i) for i in range(3)]
 
 
 def snapshot(m):
@@ -48,24 +55,40 @@ def snapshot(m):
             "results": {k: float(v) for k, v in m.results().items()}}
 
 
-def main():
-    mode, out = sys.argv[1], sys.argv[2]
-    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    m = build(B_LOCAL)
-    xs = [x[rank * B_LOCAL:(rank + 1) * B_LOCAL] for x in batches(world)]
+def run(m, xs, mode):
+    """The sequence both the ranks and the single-process reference execute: step on xs[0], step on xs[1]
+    (eager, or: capture = one eager warm-up step on xs[0], then the captured step replayed on xs[1]), then
+    one forward-only EMA call of level 0 on xs[2]. Snapshots after the first step, the second step and the
+    forward."""
+    res = {}
     if mode == "eager":
         m.train_step(xs[0])
+        torch.cuda.synchronize()
+        res["step1"] = snapshot(m)
         m.train_step(xs[1])
-    else:  # one eager warm-up step on xs[0], then the captured step replayed on xs[1]
+    else:
         m.capture_train_step(xs[0], warmup=1)
+        torch.cuda.synchronize()
+        res["step1"] = snapshot(m)
         m.train_step(xs[1])
     torch.cuda.synchronize()
-    res = {"steps": snapshot(m)}
+    res["steps"] = snapshot(m)
     m.vqvaes[0](xs[2], training=True)  # forward-only EMA: global statistics under DP
     torch.cuda.synchronize()
     res["forward"] = snapshot(m)
+    return res
+
+
+def main():
+    mode, out = sys.argv[1], sys.argv[2]
+    config = sys.argv[3] if len(sys.argv) > 3 else "cfg1"
+    dtype = sys.argv[4] if len(sys.argv) > 4 else "fp32"
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = build(B_LOCAL, config=config, dtype=dtype)
+    xs = [x[rank * B_LOCAL:(rank + 1) * B_LOCAL] for x in batches(world, config)]
+    res = run(m, xs, mode)
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

@@ -1,20 +1,40 @@
 """The product's data-parallel step: two ranks (gloo, both on cuda:0) drive VQVAE with a
 process group — eager, and graph-captured (two hipGraphs around the eager all_reduce) — and must end where
-a single process training on the concatenated global batch ends: code counts bitwise, the same global reset rows,
-EMA sums / codebooks / weights / Adam moments within fp32 rounding of the different summation grouping
-(rank-local sums then the all_reduce), metrics alike; both ranks identical to each other bitwise. Then one
-forward-only `vqvaes[0](x, training=True)` (the EMA on the global batch's statistics) likewise.
+a single process training on the concatenated global batch ends. Cases: BASELINE config 1's architecture
+(fp32) and the benched architecture that the 8-GPU run executes (config 2/3: 3 levels, K = 2048, down_depth
+[3,2,2], the levels' forward/backward chains on concurrent HIP streams joined before the exchange; fp32 and
+bf16) on an 8192-frame chunk.
+
+Bounds (vs the single process on the global batch):
+  after step 1 — every item's forward / backward rows are computed identically wherever the item sits, so
+    code counts and the global reset rows are bitwise equal; the EMA sums and the exchanged gradient differ
+    only by the summation grouping (rank-local fixed-order sums, then the all_reduce): EMA sums rel 1e-6,
+    gradients rel 2e-6 (fp32) / 1e-5 (bf16, fp32 accumulation of bf16 products), max-norm relative;
+  after step 2 and the forward-only EMA call — step 2 runs on weights that differ in their last bits, so a
+    row whose two nearest codes lie within that rounding may take the other code (Keras Adam's first steps
+    move each weight by ~ +-lr whatever the gradient's size, so an element whose gradient is pure rounding
+    noise can move the other way: measured max |delta w| 1.4e-3 after step 2); bounds: codes changed on
+    <= 0.5 % of rows (fp32) / 2 % (bf16, where the fp32 master weights' last-bit differences also flip the
+    bf16 rounding of a few weights), the number is printed; the EMA sums of every code whose count did not
+    change L2 1e-3 / 2e-2; reset rows rel 2e-3 / 2e-2; weights within two Keras Adam updates
+    (|delta w| <= 2 lr) and relative L2 3e-3; with no row moved in fp32: weights / Adam moments / codebooks
+    rel 1e-5 and N_t bitwise;
+  always — the ranks' replicas are bitwise identical (weights, codebooks, EMA statistics).
+Also: bench.py itself under torchrun with 2 gloo ranks on the one GPU (the DP branch of the driver's
+command: split graphs around the exchange, max-over-ranks timing): one JSON line with value = 2 x
+value_per_gpu and dp2 in its config.
 """
+import json
 import os
 import socket
 import subprocess
 import sys
 
-import numpy as np
 import pytest
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 sys.path.insert(0, HERE)
 import dp_worker as W  # noqa: E402
 
@@ -29,31 +49,32 @@ def _port():
     return p
 
 
-def _run_ranks(mode, tmp_path, world=2):
+def _run_ranks(mode, tmp_path, config, dtype, world=2):
     port = _port()
     procs, outs = [], []
     for r in range(world):
-        out = str(tmp_path / f"{mode}_rank{r}.pt")
+        out = str(tmp_path / f"{mode}_{config}_{dtype}_rank{r}.pt")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out, config, dtype],
+                                      env=env))
         outs.append(out)
     for p in procs:
         assert p.wait(timeout=300) == 0
     return [torch.load(o, weights_only=True) for o in outs]
 
 
-def _single(world=2):
-    m = W.build(W.B_LOCAL * world)
-    xs = W.batches(world)
-    m.train_step(xs[0])
-    m.train_step(xs[1])
-    torch.cuda.synchronize()
-    res = {"steps": W.snapshot(m)}
-    m.vqvaes[0](xs[2], training=True)
-    torch.cuda.synchronize()
-    res["forward"] = W.snapshot(m)
-    return res
+_SINGLE = {}
+
+
+def _single(config, dtype, world=2):
+    key = (config, dtype)
+    if key not in _SINGLE:
+        m = W.build(W.B_LOCAL * world, config=config, dtype=dtype)
+        _SINGLE[key] = W.run(m, W.batches(world, config), "eager")
+        del m
+        torch.cuda.empty_cache()
+    return _SINGLE[key]
 
 
 def _rel(a, b):
@@ -61,39 +82,131 @@ def _rel(a, b):
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph"])
-def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode):
-    ranks = _run_ranks(mode, tmp_path)
-    ref = _single()
-    K, D = W.CFG["num_embeddings"], W.CFG["latent_dim"]
-    assert torch.equal(ranks[0]["steps"]["stats"], ranks[1]["steps"]["stats"])  # incl. the exchanged losses
-    for phase in ("steps", "forward"):
-        r0, r1, s = ranks[0][phase], ranks[1][phase], ref[phase]
-        # replicas identical (the EMA statistics; after the forward-only call the loss slots hold each rank's
-        # local commitment loss, as vqvaes[l].losses does in the reference)
-        nst = 2 * K * D + K
-        assert torch.equal(r0["weights"], r1["weights"]) and torch.equal(r0["stats"][:nst], r1["stats"][:nst])
-        for a, b in zip(r0["vq"], r1["vq"]):
-            assert all(torch.equal(a[k], b[k]) for k in ("embeddings", "m_t", "N_t")) and a["calls"] == b["calls"]
-        # vs one process on the global batch
-        st, ss = r0["stats"], s["stats"]
-        m_sum, n_sum, RT = st[:K * D], st[K * D:K * D + K], st[K * D + K:2 * K * D + K]
-        assert torch.equal(n_sum, ss[K * D:K * D + K]), f"{phase}: code counts"
-        # the same global rows selected (their values carry step 1's fp32 weight differences)
-        assert _rel(RT, ss[K * D + K:2 * K * D + K]) < 1e-5, f"{phase}: reset rows"
-        assert _rel(m_sum, ss[:K * D]) < 1e-6, f"{phase}: EMA sums"
-        if phase == "steps":
-            # the exchanged gradient (sum over ranks of rank-mean gradients) = world x the global-batch mean
-            # gradient, to fp32 rounding of the different summation grouping
-            assert _rel(r0["grads"] / 2, s["grads"]) < 2e-6, f"{phase}: gradients"
+def _l2(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+CASES = [("cfg1", "fp32"), ("cfg2_short", "fp32"), ("cfg2_short", "bf16")]
+
+
+def _compare(r0, r1, s, K, D, L, phase, bf16):
+    """-> (report lines, failures) of one phase's rank-0 / rank-1 / single-process snapshots."""
+    lr = 1e-3  # Keras Adam default (vqa_optim.Adam)
+    nst = 2 * K * D + K  # one level's stats region: m_sumT, n_sum, RT
+    rep, bad = [], []
+
+    def check(ok, msg):
+        rep.append(("ok   " if ok else "FAIL ") + msg)
+        if not ok:
+            bad.append(msg)
+
+    # replicas identical (the EMA statistics; after the forward-only call the loss slots hold each rank's local
+    # commitment loss, as vqvaes[l].losses does in the reference)
+    check(torch.equal(r0["weights"], r1["weights"]), "replica weights bitwise")
+    check(torch.equal(r0["stats"][:L * nst], r1["stats"][:L * nst]), "replica EMA statistics bitwise")
+    check(all(torch.equal(a[k], b[k]) and a["calls"] == b["calls"] for a, b in zip(r0["vq"], r1["vq"])
+              for k in ("embeddings", "m_t", "N_t")), "replica codebooks bitwise")
+    if phase != "forward":
+        check(torch.equal(r0["stats"], r1["stats"]), "replica exchanged losses bitwise")
+    # vs one process on the global batch, level by level (the forward-only call refreshes level 0 only)
+    flips = {}
+    for l in (range(1) if phase == "forward" else range(L)):
+        st, ss = r0["stats"][l * nst:(l + 1) * nst], s["stats"][l * nst:(l + 1) * nst]
+        m_sum, n_sum, RT = st[:K * D], st[K * D:K * D + K], st[K * D + K:]
+        rows = float(ss[K * D:K * D + K].sum())
+        moved = float((n_sum - ss[K * D:K * D + K]).abs().sum()) / 2
+        flips[l] = moved
+        if phase == "step1":
+            check(moved == 0, f"level {l}: code counts bitwise ({rows:.0f} rows)")
+            check(torch.equal(RT, ss[K * D + K:]), f"level {l}: global reset rows bitwise")
+            e = _rel(m_sum, ss[:K * D])
+            check(e < 1e-6, f"level {l}: EMA sums rel {e:.2e} < 1e-6")
+        else:
+            # step 2 runs on weights that differ in their last bits (summation grouping of step 1's gradient):
+            # a row whose two nearest codes are within that rounding may take the other one
+            lim = 2e-2 if bf16 else 5e-3
+            check(moved <= lim * rows, f"level {l}: {moved:.0f} of {rows:.0f} rows changed code (<= {lim:g})")
+            e = _rel(RT, ss[K * D + K:])
+            check(e < (2e-2 if bf16 else 2e-3), f"level {l}: reset rows rel {e:.2e}")
+            # the EMA sums of every code whose count is unchanged (the moved rows are accounted for above)
+            same = n_sum == ss[K * D:K * D + K]
+            e = _l2(m_sum.view(K, D)[same], ss[:K * D].view(K, D)[same])
+            tol = 1e-6 if moved == 0 and not bf16 else (2e-2 if bf16 else 1e-3)
+            check(e < tol, f"level {l}: EMA sums of the {int(same.sum())} codes with unchanged counts, L2 {e:.2e}")
+    if phase == "step1":
+        # the exchanged gradient (sum over ranks of rank-mean gradients) = world x the global-batch mean
+        # gradient, to fp32 rounding of the different summation grouping
+        e, tol = _rel(r0["grads"] / 2, s["grads"]), (1e-5 if bf16 else 2e-6)
+        check(e < tol, f"exchanged gradient rel {e:.2e} < {tol:g}")
+    exact_path = phase == "step1" or (not bf16 and not any(flips.values()))
+    if exact_path:
         # Adam normalises each element by sqrt(v): an element whose gradient nearly cancels across items keeps
         # its absolute rounding noise but has a small sqrt(v), so a 1e-7-relative gradient difference becomes
-        # up to ~1e-3 of that element's update (Keras default lr = 1e-3 per step), i.e. a few 1e-6 of max|w|
-        assert _rel(r0["weights"], s["weights"]) < 1e-5, f"{phase}: weights"
-        if phase == "steps":
-            assert _rel(r0["adam_m"], s["adam_m"]) < 1e-5 and _rel(r0["adam_v"], s["adam_v"]) < 1e-5
-        for a, b in zip(r0["vq"], s["vq"]):
-            assert torch.equal(a["N_t"], b["N_t"]) and a["calls"] == b["calls"]
-            assert _rel(a["embeddings"], b["embeddings"]) < 1e-5 and _rel(a["m_t"], b["m_t"]) < 1e-5
-        for k, v in s["results"].items():
-            assert abs(r0["results"][k] - v) <= 1e-5 * max(abs(v), 1e-3), f"{phase} {k}: {r0['results'][k]} vs {v}"
+        # up to ~1e-3 of that element's update (lr = 1e-3 per step), i.e. a few 1e-6 of max|w|
+        e = _rel(r0["weights"], s["weights"])
+        check(e < 1e-5, f"weights rel {e:.2e} < 1e-5")
+        if phase != "forward":
+            e = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"]))
+            check(e < 1e-5, f"Adam moments rel {e:.2e} < 1e-5")
+    else:
+        dw = float((r0["weights"] - s["weights"]).abs().max())
+        check(dw <= 2 * lr * 1.01, f"max |delta w| {dw:.2e} <= two Adam updates ({2 * lr:g})")
+        e = _l2(r0["weights"], s["weights"])
+        check(e < 3e-3, f"weights relative L2 {e:.2e} < 3e-3")
+    for l, (a, b) in enumerate(zip(r0["vq"], s["vq"])):
+        check(a["calls"] == b["calls"], f"level {l}: reset counter")
+        if exact_path:
+            check(torch.equal(a["N_t"], b["N_t"]), f"level {l}: N_t bitwise")
+            e = max(_rel(a["embeddings"], b["embeddings"]), _rel(a["m_t"], b["m_t"]))
+            check(e < 1e-5, f"level {l}: codebook / m_t rel {e:.2e}")
+        else:
+            e = max(_l2(a["m_t"], b["m_t"]), _l2(a["N_t"], b["N_t"]))
+            check(e < 1e-2, f"level {l}: m_t / N_t relative L2 {e:.2e}")
+    rtol = 1e-5 if exact_path else 2e-2
+    worst = 0.0
+    for k, v in s["results"].items():
+        if not exact_path and ("usage" in k or "entropy" in k):
+            continue
+        worst = max(worst, abs(r0["results"][k] - v) / max(abs(v), 1e-3))
+    check(worst <= rtol, f"metrics rel {worst:.2e} <= {rtol:g}")
+    return rep, bad
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+@pytest.mark.parametrize("config,dtype", CASES)
+def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode, config, dtype):
+    cfg = W.CONFIGS[config]
+    K, D, L = cfg["num_embeddings"], cfg["latent_dim"], cfg["levels"]
+    ranks = _run_ranks(mode, tmp_path, config, dtype)
+    ref = _single(config, dtype)
+    failures = []
+    for phase in ("step1", "steps", "forward"):
+        rep, bad = _compare(ranks[0][phase], ranks[1][phase], ref[phase], K, D, L, phase, dtype == "bf16")
+        print(f"--- {config} {dtype} {mode} {phase}")
+        print("\n".join(rep))
+        failures += [f"{phase}: {b}" for b in bad]
+    assert not failures, failures
+
+
+@pytest.mark.timeout(600)
+def test_bench_py_dp2_gloo_one_gpu(cuda):
+    """The driver's N > 1 command form (torch.distributed.run, one process per rank, bench.py --gpus 2) with
+    VQA_DIST_BACKEND=gloo so both ranks share the one GPU: the split-graph DP branch, barrier + max-over-ranks
+    timing and the JSON line."""
+    port = _port()
+    env = dict(os.environ, VQA_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch", "2", "--seq", "8192", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert abs(out["value_per_gpu"] * 2 - out["value"]) <= 1e-6 * out["value"] + 0.2
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    want = 2 * 2 * 8192 / (out["ms_per_step"] * 1e-3)  # 2 ranks x batch 2 x 8192 frames per step
+    assert abs(out["value"] - want) <= 1e-3 * want

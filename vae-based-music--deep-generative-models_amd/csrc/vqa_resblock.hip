@@ -21,6 +21,7 @@
 #include "vqa_mfma.h"
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 
 namespace vqa {
 
@@ -159,7 +160,6 @@ template <> __device__ __forceinline__ void pos8<float>(const float* p, bool (&m
 }
 
 // bf16 epilogue helpers on packed bits (two bf16 per dword, packed integer ops: one instruction per pair)
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
 // two floats rounded to bf16 by ONE v_cvt_pk_bf16_f32 (a vector conversion; element-wise casts of a bf16x8
 // were emitted as one cvt per value plus a v_perm per pair)
@@ -172,11 +172,15 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
 __device__ __forceinline__ uint4 bf16_bits(f32x4 lo, f32x4 hi) {
   return uint4{pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]), pk_bf16(hi[0], hi[1]), pk_bf16(hi[2], hi[3])};
 }
-// d * (r > 0) per bf16 where r >= 0 (a relu'd tensor): d's bits times min(r's bits, 1) (v_pk_min_u16 + v_pk_mul_lo_u16)
+// d * (r > 0) per bf16 where r >= 0 (a relu'd tensor): d's bits times min(r's bits, 1) (v_pk_min_u16 + v_pk_mul_lo_u16).
+// Written as two asm statements: from the builtin form the compiler re-derived a per-half compare + select
+// (v_cmp_ne_u16 / v_cndmask / v_lshrrev / v_perm and hazard s_nops: ~6 instructions per dword instead of 2).
+// Plain VALU operands: no memory operation and no wait state inside the strings (cdna_hip_programming.md §5.7).
 __device__ __forceinline__ unsigned mask_pos_pk(unsigned d, unsigned r) {
-  const u16x2 one = {1, 1};
-  const u16x2 m = __builtin_elementwise_min(__builtin_bit_cast(u16x2, r), one);
-  return __builtin_bit_cast(unsigned, __builtin_bit_cast(u16x2, d) * m);
+  unsigned m, o;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(r), "s"(0x00010001u));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(o) : "v"(d), "v"(m));
+  return o;
 }
 __device__ __forceinline__ uint4 mask_pos8(uint4 d, uint4 r) {
   return uint4{mask_pos_pk(d.x, r.x), mask_pos_pk(d.y, r.y), mask_pos_pk(d.z, r.z), mask_pos_pk(d.w, r.w)};
@@ -214,8 +218,10 @@ template <class T, int PV>
 struct Rows32Buf {
   static constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC, ROWB = RC * (int)sizeof(T);
   uint4 v[PV];
-  int goff[PV], loff[PV];  // byte offset from the tile's first row; LDS element offset (-1: none)
-  __device__ __forceinline__ void init(int nrows) {
+  int goff[PV], loff[PV];  // byte offset from the tile's first row; LDS element offset from the buffer
+  // chunks past the tile's rows load zeros (out-of-range offset) and store them to a trash slot `trash`
+  // elements from the buffer: every lane stores, so the staging needs no EXEC-masked branches
+  __device__ __forceinline__ void init(int nrows, int trash) {
     constexpr int XS = RC + 16 / (int)sizeof(T);
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
@@ -231,7 +237,7 @@ struct Rows32Buf {
       }
       const bool in = rr < nrows;
       goff[i] = in ? rr * ROWB + q * 16 : kRsOOB;
-      loff[i] = in ? rr * XS + q * VEC : -1;
+      loff[i] = in ? rr * XS + q * VEC : trash;
     }
   }
   __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int row0) {
@@ -243,15 +249,14 @@ struct Rows32Buf {
   template <bool RELU>
   __device__ __forceinline__ void store(T* dst) const {
 #pragma unroll
-    for (int i = 0; i < PV; ++i)
-      if (loff[i] >= 0) {
-        uint4 w = v[i];
-        if constexpr (RELU) {
-          if constexpr (sizeof(T) == 2) w = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, w)));
-          else relu_bits<T>(w);
-        }
-        *(uint4*)(dst + loff[i]) = w;
+    for (int i = 0; i < PV; ++i) {
+      uint4 w = v[i];
+      if constexpr (RELU) {
+        if constexpr (sizeof(T) == 2) w = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, w)));
+        else relu_bits<T>(w);
       }
+      *(uint4*)(dst + loff[i]) = w;
+    }
   }
 };
 
@@ -397,7 +402,7 @@ void resblock_fwd_kernel(ResArgs a) {
   auto item_x = [&](int tile) { return rs_rsrc((const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC, ibytes); };
   auto row0 = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RT - 1 - d; };
   Rows32Buf<T, rs_pv<T>()> nx;
-  nx.init(XR);
+  nx.init(XR, (XR + HR) * XS);  // trash row after H
   nx.load(item_x(tbeg), row0(tbeg));
   nx.template store<false>(X);
   if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1));
@@ -522,8 +527,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     by.load(rs_rsrc((const T*)a.dy + o, ibytes), tstart(tile) - d - 1);
   };
   Rows32Buf<T, rs_pv<T>()> nx, ny;
-  nx.init(XR);
-  ny.init(YR);
+  nx.init(XR, (XR + YR + HR) * XS);  // trash row after H
+  ny.init(YR, (YR + HR) * XS);
   load_tile(nx, ny, tbeg);
   nx.template store<true>(X);
   ny.template store<false>(Y);
@@ -540,18 +545,32 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       f32x4 acc[3][2];
       auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
       conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d);
+      if constexpr (sizeof(T) == 2) {
+        // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8; the
+        // SAME-padding rows of an edge tile are zeroed on a separate (wave-uniform) path
+        auto store_h = [&](auto edge) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            if (wave + 4 * j >= nht) continue;
+            const int i = rh[j] + pn;
+            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
+                                                                                              acc[j][1] + bav[1]))));
+            if constexpr (decltype(edge)::value) {
+              const int r = t0 - d + i;
+              if (r < 0 || r >= a.T) u = uint4{0u, 0u, 0u, 0u};
+            }
+            *(uint4*)(H + i * XS + oc) = u;
+          }
+        };
+        if (interior) store_h(std::false_type{});
+        else store_h(std::true_type{});
+      } else {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= nht) continue;
         const int i = rh[j] + pn, r = t0 - d + i;
         const bool live = interior || (r >= 0 && r < a.T);
-        if constexpr (sizeof(T) == 2) {
-          // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8
-          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
-                                                                                            acc[j][1] + bav[1]))));
-          if (!interior && !live) u = uint4{0u, 0u, 0u, 0u};
-          *(uint4*)(H + i * XS + oc) = u;
-        } else {
+        {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
@@ -561,6 +580,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           }
           st8(H + i * XS + oc, v[0], v[1]);
         }
+      }
       }
     }
     __syncthreads();
@@ -686,13 +706,14 @@ static int rs_cus() {
 constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the partial rows)
 constexpr int kResMinTiles = 4;  // backward: tiles per workgroup at least (bounds the partial rows of short launches)
 
+// + one trash row for the staging chunks past a tile's rows (Rows32Buf)
 static size_t fwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = rt + 16;
-  return ((size_t)(HR + 2 * d) * s + (size_t)HR * s) * esz;
+  return ((size_t)(HR + 2 * d) * s + (size_t)HR * s + s) * esz;
 }
 static size_t bwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = round16(rt + 2 * d);
-  return ((size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s) * esz;
+  return ((size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s + s) * esz;
 }
 
 static int set_lds(const void* fn, size_t bytes) {

@@ -14,7 +14,7 @@ has exactly one collective; with ~5.5 MB at cfg2 it is latency-bound on xGMI (~t
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence
+from typing import Dict, Sequence
 
 import torch
 import torch.distributed as dist
@@ -49,15 +49,9 @@ def exchange(bucket: torch.Tensor, group=None) -> int:
     """Sum the bucket over ranks (no-op on one rank). Returns the world size (grad scale = 1/W)."""
     w = world_size(group)
     if w > 1:
-        if bucket.is_cuda and dist.get_backend(group) != "nccl":
-            # host backends (gloo: the CPU rehearsal / tests of the DP path): stage through host memory
-            # explicitly, ordered after every kernel that wrote the bucket
-            torch.cuda.current_stream(bucket.device).synchronize()
-            host = bucket.cpu()
-            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-            bucket.copy_(host)
-        else:
-            dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)  # RCCL over xGMI
+        # RCCL over xGMI ("nccl"); the gloo rehearsal / tests pass the same device bucket (torch's gloo stages
+        # it through pinned host memory on its own streams, ordered after the current stream like RCCL's)
+        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return w
 
 
