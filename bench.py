@@ -219,6 +219,13 @@ def main():
         except Exception:
             pmc = {}
     traffic = pmc.get("per_launch_bytes")
+    # provenance of the counter file: a traffic figure read from another library build is flagged stale
+    lib_sha = None
+    try:
+        import hashlib
+        lib_sha = hashlib.sha256(open(V.LIB_PATH, "rb").read()).hexdigest()
+    except Exception:
+        pass
     avg_us = us_total / max(n_launch, 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": DOMINANT,
@@ -226,7 +233,11 @@ def main():
             "algorithmic_bytes_per_launch": int(nbytes / max(n_launch, 1)),
             "compulsory_bytes_per_launch": int(cbytes / max(n_launch, 1)),
             "compulsory_GBps": round(compulsory, 1), "compulsory_frac": round(compulsory / HBM_PEAK_GBS, 4),
-            "kernel_ms_per_step": round(us_total / 1e3, 3)}
+            "kernel_ms_per_step": round(us_total / 1e3, 3),
+            "traffic_source": {"file": os.path.relpath(a.pmc_json, ROOT) if pmc else None,
+                               "commit": pmc.get("commit"), "measured_utc": pmc.get("measured_utc"),
+                               "lib_sha256": pmc.get("lib_sha256"), "loaded_lib_sha256": lib_sha,
+                               "same_library": bool(lib_sha and pmc.get("lib_sha256") == lib_sha)}}
     if traffic and avg_us > 0:
         # measured HBM bytes (PMC, profiles/) over the live average launch time: the real bandwidth fraction
         roof["traffic_GBps"] = round(traffic / (avg_us * 1e-6) / 1e9, 1)
@@ -248,6 +259,8 @@ def main():
         # value_per_gpu: the metric's per-GPU reading (B_per_gpu * T * steps / wall-seconds)
         value = a.batch * a.seq * a.steps * world / elapsed
         out = {"metric": METRIC, "value": round(value, 1), "value_per_gpu": round(value / world, 1),
+               "value_is": "whole-job aggregate over n_gpus (the bench contract: total audio-samples/s of all ranks); "
+                           "value_per_gpu is the metric's per-GPU reading",
                "unit": "audio-samples/s", "n_gpus": world,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,

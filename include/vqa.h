@@ -223,9 +223,17 @@ int vqa_mse_loss(const float* x, const float* r, const float* extra_grad, float*
 size_t vqa_mse_loss_workspace(int64_t n);
 /* Keras 2.7 Adam (vqvae.py:144, compile at :362; TF ApplyAdam): t = *step + 1,
  * alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g*s - m)(1-b1); v += ((g*s)^2 - v)(1-b2);
- * w -= alpha*m/(sqrt(v)+eps), with s = grad_scale. Does not touch *step. */
+ * w -= alpha*m/(sqrt(v)+eps), with s = grad_scale. Does not touch *step. lr_dev (nullable): a device scalar
+ * that replaces lr (a LearningRateSchedule's value for this step, written by vqa_lr_schedule). */
 int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, const int64_t* step, float lr,
-                   float beta1, float beta2, float eps, float grad_scale, vqa_stream_t stream);
+                   const float* lr_dev, float beta1, float beta2, float eps, float grad_scale, vqa_stream_t stream);
+/* keras LearningRateSchedule at the optimizer's device step counter (OptimizerV2._decayed_lr: schedule(float(
+ * iterations)), before the step's increment): *lr = f(*step), so a captured train step replays with the right rate.
+ * kind 0: p0. kind 1, CustomSchedule (src/transformer/multi_head_attention.py:82-101): p0 = rsqrt(d_model),
+ * p1 = warmup_steps^-1.5: p0 * min(rsqrt(s), s * p1). kind 2, keras ExponentialDecay: p0 = initial rate,
+ * p1 = decay_steps, p2 = decay_rate, p3 = staircase: p0 * p2^(s / p1) (exponent floored when staircase). */
+int vqa_lr_schedule(const int64_t* step, float* lr, int kind, float p0, float p1, float p2, float p3,
+                    vqa_stream_t stream);
 /* The train step's metric trackers in one launch (replaces update_metrics, vqvae.py:262-304, and the VQ
  * trackers, VectorQuantizer.py:149-159): macc is (4 + 7*levels) x (total, count) — rows loss, recon_loss,
  * vqvae_loss, spectral_loss, then per level level/recon/vq/spectral loss, batch usage, usage, entropy;
@@ -315,20 +323,23 @@ int vqa_seqlin_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, f
 /* autoregressive_fmha.py:119-151: out = table[tokens] (row 0 <- ycond when given) * scale + pos[t]; keras
  * Dropout(rate) with a counter-based mask (seed, and the device step counter when given, so a replayed graph
  * draws a new mask each step); + xcond (N, T, W) when given. The mask is vqa_dropout's over the flat
- * (N, T, W) index with salt VQA_EMB_DROPOUT_SALT: the gradient of the dropout is vqa_dropout(dx, N*T*W, rate,
- * seed, VQA_EMB_DROPOUT_SALT, counter). */
+ * (N, T, W) index (+ elem_offset: under data parallelism the rank's first global index, rank * N*T*W, so the
+ * ranks draw the single-process mask of the global batch) with salt VQA_EMB_DROPOUT_SALT: the gradient of the
+ * dropout is vqa_dropout(dx, N*T*W, rate, seed, VQA_EMB_DROPOUT_SALT, elem_offset, counter). */
 #define VQA_EMB_DROPOUT_SALT 0x454d42ull
 int vqa_prior_embed_fwd(const float* table, const float* pos, const int64_t* tokens, const float* ycond,
                         const void* xcond, void* out, int N, int T, int W, int bins, float scale, float rate,
-                        uint64_t seed, const int64_t* counter, int dtype, vqa_stream_t stream);
+                        uint64_t seed, int64_t elem_offset, const int64_t* counter, int dtype, vqa_stream_t stream);
 /* out[i] (+)= sum_{n < nout} x[n*ostride + i], i < inner (fp32 out, fixed order): positional-embedding and
  * bias gradients. */
 int vqa_colsum(const void* x, float* out, int nout, int64_t ostride, int64_t inner, int accumulate, int dtype,
                vqa_stream_t stream);
 int vqa_axpy(const void* x, const void* y, void* z, int64_t n, int dtype, vqa_stream_t stream); /* z = x + y */
-/* keras Dropout(rate) in place: x * 1/(1-rate) where uniform(seed, salt, i) >= rate, else 0. */
-int vqa_dropout(void* x, int64_t n, float rate, uint64_t seed, uint64_t salt, const int64_t* counter, int dtype,
-                vqa_stream_t stream);
+/* keras Dropout(rate) in place (src/transformer/transformer.py:31-33, autoregressive_fmha.py:151):
+ * x * 1/(1-rate) where uniform(seed, salt, elem_offset + i) >= rate, else 0. elem_offset: the global flat index of
+ * x[0] (data parallel: rank * n), so DP ranks apply the single-process mask of the global batch. */
+int vqa_dropout(void* x, int64_t n, float rate, uint64_t seed, uint64_t salt, int64_t elem_offset,
+                const int64_t* counter, int dtype, vqa_stream_t stream);
 int vqa_scale_f32(float* x, int64_t n, float s, vqa_stream_t stream);
 /* prior.py:262-290 teacher forcing: latent = [start, codes[:-1]]; pred = [start, amax[:-1]];
  * out = m ? pred : latent, m = mask[r] (uint8, when given) or uniform(seed, step + *counter, row_offset + r)
@@ -371,7 +382,10 @@ int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, float* out,
  * walks `steps` positions with a key/value cache, z = logits + Gumbel(uniform(seed, sample, step, bin)),
  * next token = argmax z. tokens (N, steps+1) int64 with tokens[:, 0] = start. Optional: ycond (N, width)
  * label embedding for position 0, xcond (N, ctx, width) fp32 upper-level conditioning, forced (N, steps+1)
- * input tokens (teacher-forced check), logits (N, steps, bins) output. width 128, attention width 32. */
+ * input tokens (teacher-forced check), logits (N, steps, bins) output. width 128, attention width 32.
+ * out_kernel is (width, out_ld) row-major with out_ld >= bins a multiple of 4 and out_bias has out_ld entries
+ * (a vocabulary that is not a multiple of 4, e.g. the sampler's default 513 bins, is passed zero-padded; the
+ * padded columns are never sampled). */
 typedef struct {
   const float *ln1_gamma, *ln1_beta, *qkv_kernel, *qkv_bias, *query_kernel, *query_bias, *key_kernel, *key_bias,
       *value_kernel, *value_bias, *out_kernel, *out_bias, *proj_kernel, *proj_bias, *ln2_gamma, *ln2_beta,
@@ -382,8 +396,8 @@ size_t vqa_prior_decode_cache_bytes(int N, int depth, int ctx);
 int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const float* x_embedding, const float* pos_embedding,
                      const float* out_kernel, const float* out_bias, const float* ycond, const float* xcond,
                      const int64_t* forced, float* logits, int64_t* tokens, void* cache, size_t cache_bytes, int N,
-                     int steps, int ctx, int width, int heads, int blocks, int bins, int64_t start, uint64_t seed,
-                     vqa_stream_t stream);
+                     int steps, int ctx, int width, int heads, int blocks, int bins, int out_ld, int64_t start,
+                     uint64_t seed, vqa_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,7 @@
 Runs Prior.train_step with a torch.distributed process group (gloo, every rank on cuda:0) on its shard of the
 global batch — eager, or as two captured hipGraphs around the eager all_reduce — and saves the state.
     python tests/prior_dp_worker.py MODE OUT   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment)
+MODE: eager | graph, with the suffixes _cond (upsampler form) and / or _drop (dropout 0.1).
 """
 import os
 import sys
@@ -21,14 +22,15 @@ def cfg():
     return P.PriorConfig(bins=64, ctx=256, width=128, depth=3, heads=2, blocks=4, attn_stacks=1)
 
 
-def build(process_group=None, cond=False):
+def build(process_group=None, cond=False, drop=False):
     """cond: the upsampler form — level 0 of 2 with ConditionerNet on the level above (Sampler.py:24) and genre
-    labels (LabelConditioner), every parameter from the seeded store initialisation."""
+    labels (LabelConditioner), every parameter from the seeded store initialisation. drop: the reference's
+    default dropout rate 0.1 (embedding and every residual block's attention output)."""
     from oracle import prior_ref as P
     from prior import Prior
     c = cfg()
     pk = dict(width=c.width, depth=c.depth, heads=c.heads, blocks=c.blocks, attn_stacks=c.attn_stacks,
-              drop_out_rate=0.0)
+              drop_out_rate=0.1 if drop else 0.0)
     if cond:
         ck = dict(dilation_factor=3, dilation_cycle=4, residual_width=32, residual_depth=8)
         return Prior(0, [(c.ctx,), (c.ctx // 4,)], c.bins, [3, 2], [2, 2], None, pk, ck, genre_classes=10,
@@ -76,9 +78,9 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cond = mode.endswith("_cond")
-    mode = mode.replace("_cond", "")
-    pr = build(dist.group.WORLD, cond)
+    cond, drop = "_cond" in mode, "_drop" in mode
+    mode = mode.split("_")[0]
+    pr = build(dist.group.WORLD, cond, drop)
     xs = [shard(x, rank) for x in batches(world, cond)]
     if mode == "eager":
         pr.train_step(xs[0])

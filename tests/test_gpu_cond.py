@@ -59,20 +59,74 @@ def test_conditioner_forward_backward_vs_oracle(cuda, dtype, tol):
         assert np.median(list(errs.values())) < 1e-5
     else:
         # bf16 activations round every one of the 24 residual blocks' pre-activations, so ReLU masks near 0
-        # differ from fp64's and the gradient drifts through the depth (0.05 at the LayerNorm end, ~0.2 at the
-        # embedding, measured); the per-layer bf16 kernels are pinned by test_gpu_resblock / test_gpu_conv. Here:
-        # every tensor points the same way (cosine >= 0.95) and the whole gradient is within 0.3 relative L2.
+        # differ from a wider type's and the end-to-end gradient drifts through the depth. The strict bf16 check is
+        # test_conditioner_bf16_blocks_teacher_forced (every block against fp64 on its own inputs and masks);
+        # here, against the SAME network run in fp32 on the GPU: the whole gradient and every tensor's direction.
+        net32 = _net(L, torch.float32, cuda)
+        y32 = net32.forward(idx.to(cuda), save=True)
+        net32.store.grad.zero_()
+        net32.backward(dy.to(cuda).float())
+        torch.cuda.synchronize()
+        g32 = net32.store.grads()
+        errs32 = {k: _l2(got[k], g32[k]) for k in p}
+        print("bf16 vs fp32 GPU:", {k.split("/", 1)[1]: round(e, 4) for k, e in errs32.items()})
+        assert _l2(y.float(), y32) < 2e-2
         flat_got = np.concatenate([got[k].ravel() for k in p]).astype(np.float64)
-        flat_want = np.concatenate([gr.numpy().ravel() for gr in grads])
-        assert np.linalg.norm(flat_got - flat_want) / np.linalg.norm(flat_want) < 0.3
-        for k, gr in zip(p, grads):
-            a, b = got[k].ravel().astype(np.float64), gr.numpy().ravel()
+        flat_32 = np.concatenate([g32[k].ravel() for k in p]).astype(np.float64)
+        assert np.linalg.norm(flat_got - flat_32) / np.linalg.norm(flat_32) < 0.15
+        for k in p:
+            a, b = got[k].ravel().astype(np.float64), g32[k].ravel().astype(np.float64)
             cos = float(a @ b / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-30))
-            assert cos >= 0.95, f"{k}: cosine {cos:.3f}"
+            assert cos >= 0.98, f"{k}: cosine {cos:.3f} vs the fp32 network"
     # the embedding gradient: rows of unused codes are exactly zero
     used = torch.zeros(CFG["bins"], dtype=torch.bool)
     used[idx.reshape(-1)] = True
     assert (got[f"{net.name}/embedding/embeddings"][~used.numpy()] == 0).all()
+
+
+def test_conditioner_bf16_blocks_teacher_forced(cuda, monkeypatch):
+    """Every residual block of the bf16 ConditionerNet (24 fused blocks, cyclic dilations 1, 3, 9, 27) against fp64
+    autograd on the GPU's own saved input, upstream gradient and relu(h) masks: dx and all four weight gradients
+    within 1e-2 relative L2 (the bf16 roundings of dh and dx). No ReLU branch can flip, so the bound is strict."""
+    import resnet
+    from test_gpu_resblock import block_grads_fp64
+    B, L = 2, 32
+    net = _net(L, torch.bfloat16, cuda)
+    g = torch.Generator().manual_seed(5)
+    idx = torch.randint(0, CFG["bins"], (B, L), generator=g)
+    y = net.forward(idx.to(cuda), save=True)
+    dy = torch.randn(y.shape, generator=g)
+    log = []
+    orig = resnet.ResnetConv1DBlock.backward
+
+    def spy(self, d_y):
+        x = self._saved[0]
+        h, y_ = torch.empty_like(x), torch.empty_like(x)
+        V.resblock_fwd(x, self.conv_a.w, self.conv_a.b, self.conv_b.w, self.conv_b.b, y_, self.dilation, h_out=h)
+        rec = dict(blk=self, x=x.cpu(), h=h.cpu(), dy=d_y.cpu(),
+                   W={"wa": self.conv_a.w.to(torch.bfloat16).cpu(), "ba": self.conv_a.b.cpu(),
+                      "wb": self.conv_b.w.to(torch.bfloat16).cpu(), "bb": self.conv_b.b.cpu()})
+        dx = orig(self, d_y)
+        rec["dx"] = dx.cpu()
+        log.append(rec)
+        return dx
+
+    monkeypatch.setattr(resnet.ResnetConv1DBlock, "backward", spy)
+    net.store.grad.zero_()
+    net.backward(dy.to(cuda).to(torch.bfloat16))
+    torch.cuda.synchronize()
+    monkeypatch.undo()
+    assert len(log) == 24 and {r["blk"].dilation for r in log} == {1, 3, 9, 27}
+    got = net.store.grads()
+    for rec in log:
+        blk = rec["blk"]
+        want = block_grads_fp64(rec["x"], rec["dy"], rec["h"], rec["W"], blk.dilation)
+        errs = {"dx": _l2(rec["dx"], want[0])}
+        for k, gr, pn in zip(("wa", "ba", "wb", "bb"), want[1:], (f"{blk.conv_a.name}/kernel", f"{blk.conv_a.name}/bias",
+                                                                 f"{blk.conv_b.name}/kernel", f"{blk.conv_b.name}/bias")):
+            errs[k] = _l2(got[pn], gr)
+        bad = {k: e for k, e in errs.items() if not e < 1e-2}
+        assert not bad, f"{blk.conv_a.name} d={blk.dilation}: {bad}"
 
 
 def test_conditioner_call_checks_shapes(cuda):

@@ -301,6 +301,12 @@ def test_train_step_graph_replay_matches_eager(cuda):
     torch.cuda.synchronize()
     assert torch.equal(a.prior.store.flat, b.prior.store.flat)
     assert float(a.results()["loss"]) == float(b.results()["loss"])
+    # a teacher-forcing rate other than the captured one (a schedule) runs eagerly, with that rate
+    a.train_step(codes, teacher_force_rate=0.7)
+    b.train_step(codes, teacher_force_rate=0.7)
+    torch.cuda.synchronize()
+    assert torch.equal(a.prior.store.flat, b.prior.store.flat)
+    assert torch.equal(a._last_batch_input, b._last_batch_input)
 
 
 def test_decode_teacher_forced_logits_match_oracle(cuda):
@@ -330,10 +336,22 @@ def test_decode_sampling_matches_reference_sampler(cuda):
 
 
 def test_prior_test_step_and_metrics(cuda):
-    pr, _ = _prior(CFG)
-    codes = torch.randint(0, CFG.bins - 1, (2, CFG.ctx), generator=_gen(2)).cuda()
-    r = pr.test_step(codes)
-    assert 0 < float(r["loss"]) < 10 and 0 <= float(r["accuracy"]) <= 1
+    """prior.py:337-372: test_step feeds the batch's loss / accuracy into the trackers and returns their running
+    means (a keras evaluate loop over several batches reports the mean of the batches)."""
+    pr, vals = _prior(CFG)
+    g = _gen(2)
+    batches = [torch.randint(0, CFG.bins - 1, (2, CFG.ctx), generator=g) for _ in range(2)]
+    want = [P.train_step_grads(P.to_torch(vals), CFG, c, torch.zeros(2, CFG.ctx, dtype=torch.bool))[:2] for c in batches]
+    r1 = {k: float(v) for k, v in pr.test_step(batches[0].cuda()).items()}
+    r2 = {k: float(v) for k, v in pr.test_step(batches[1].cuda()).items()}
+    assert abs(r1["loss"] - want[0][0]) <= 1e-5 * want[0][0] and abs(r1["accuracy"] - want[0][1]) <= 1e-6
+    mean_loss = (want[0][0] + want[1][0]) / 2
+    assert abs(r2["loss"] - mean_loss) <= 1e-5 * mean_loss
+    assert abs(r2["accuracy"] - (want[0][1] + want[1][1]) / 2) <= 1e-6
+    assert abs(r2["perplexity(per word)"] - math.exp(r2["loss"])) <= 1e-4 * math.exp(r2["loss"])
+    for t in pr.metrics:
+        t.reset_state()
+    codes = batches[0].cuda()
     pr.train_step(codes)
     names = [t.name for t in pr.metrics]
     assert names == ["train_loss", "train_accuracy"]
@@ -362,14 +380,54 @@ def test_dropout_mask_statistics_and_determinism(cuda):
     assert abs(frac - rate) < 3e-3
     assert torch.equal(a[a != 0], torch.full_like(a[a != 0], 1.0 / (1.0 - rate)))
     assert torch.equal(a, b) and not torch.equal(a, c)
-    # the embedding's dropout: same statistics on (table row * scale + pos)
+    # data parallel: a shard dropped with its global element offset is that slice of the full tensor's mask
+    h = x.numel() // 2
+    shard = x[h:].clone()
+    V.dropout_(shard, rate, 7, 3, ctr, elem_offset=h)
+    torch.cuda.synchronize()
+    assert torch.equal(shard, c[h:])
+    # the embedding's dropout: same statistics on (table row * scale + pos), and the same offset rule
     tok = torch.zeros(4, 4096, dtype=torch.int64, device="cuda")
     table = torch.ones(8, 128, device="cuda")
     pos = torch.zeros(4096, 128, device="cuda")
     out = torch.empty(4, 4096, 128, device="cuda")
     V.prior_embed_fwd(table, pos, tok, out, 1.0, rate=rate, seed=5)
+    out2 = torch.empty(2, 4096, 128, device="cuda")
+    V.prior_embed_fwd(table, pos, tok[2:].contiguous(), out2, 1.0, rate=rate, seed=5, elem_offset=2 * 4096 * 128)
     torch.cuda.synchronize()
     assert abs(float((out == 0).float().mean()) - rate) < 3e-3
+    assert torch.equal(out2, out[2:])
+
+
+def test_conditioning_shapes_are_checked(cuda):
+    """autoregressive_fmha.py:145-148 asserts x_cond is [n_samples, max_length, d_model]: the wrappers refuse any
+    x_cond / y_cond / forced that the kernels would read past (batch mismatch, too few positions, wrong width)
+    with ValueError before a pointer reaches the device."""
+    m, _ = _model(CFG)
+    tok = torch.randint(0, CFG.bins, (2, CFG.ctx), generator=_gen(3))
+    W = CFG.width
+    bad_x = [torch.zeros(3, CFG.ctx, W), torch.zeros(2, CFG.ctx - 1, W), torch.zeros(2, CFG.ctx, W // 2)]
+    for xc in bad_x:
+        with pytest.raises(ValueError):
+            m(tok, x_cond=xc.cuda())
+    for yc in (torch.zeros(3, W), torch.zeros(2, W + 1)):
+        with pytest.raises(ValueError):
+            m(tok, y_cond=yc.cuda())
+    L = 40
+    for xc in (torch.zeros(3, CFG.ctx, W), torch.zeros(2, L - 1, W), torch.zeros(2, CFG.ctx, W - 4)):
+        with pytest.raises(ValueError):
+            m.sample(2, max_length=L, x_cond=xc.cuda())
+    with pytest.raises(ValueError):
+        m.sample(2, max_length=L, y_cond=torch.zeros(1, W).cuda())
+    for forced in (torch.zeros(2, L, dtype=torch.int64), torch.zeros(1, L + 1, dtype=torch.int64)):
+        with pytest.raises(ValueError):
+            m.sample(2, max_length=L, forced=forced.cuda())
+    with pytest.raises(ValueError):
+        m.sample(2, max_length=CFG.ctx + 1)
+    # the accepted forms still run: x_cond longer than the window is cut to it
+    m.sample(2, max_length=L, x_cond=torch.zeros(2, CFG.ctx, W).cuda(), y_cond=torch.zeros(2, 1, W).cuda())
+    m(tok, x_cond=torch.zeros(2, CFG.ctx, W).cuda())
+    torch.cuda.synchronize()
 
 
 def test_conditioned_logits_and_decode_match_oracle(cuda):

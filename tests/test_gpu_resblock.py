@@ -134,17 +134,42 @@ def _unfused_bwd(p, d, h):
     return dx0, ref
 
 
+def block_grads_fp64(x, dy, h_gpu, W, d):
+    """fp64 autograd of resnet.py:7-29 on the GPU's own bf16 inputs, with the ReLU' masks of the GPU's relu(h)
+    (the weights as the kernels use them: bf16-rounded kernels, fp32 biases). -> (dx, dW_a, db_a, dW_b, db_b)."""
+    x, dy = x.double().cpu(), dy.double().cpu()
+    Wv = {k: W[k].double().cpu().clone().requires_grad_(True) for k in ("wa", "ba", "wb", "bb")}
+    xv = x.clone().requires_grad_(True)
+    hh = ref_conv(xv * (x > 0), Wv["wa"], Wv["ba"], 1, d)
+    y = xv + ref_conv(hh * (h_gpu.double().cpu() > 0), Wv["wb"], Wv["bb"], 1, 1)
+    return torch.autograd.grad((y * dy).sum(), [xv] + [Wv[k] for k in ("wa", "ba", "wb", "bb")])
+
+
+def bf16_weights(p):
+    """the kernels stage the fp32 conv kernels as bf16 MFMA operands; biases stay fp32"""
+    return {"wa": p["wa"].to(torch.bfloat16), "ba": p["ba"], "wb": p["wb"].to(torch.bfloat16), "bb": p["bb"]}
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("T,d", [(32768, 27), (32768, 1), (8192, 9), (512, 3)])
 def test_full_size_cfg2(cuda, T, d):
     """cfg2 shapes (B = 32, bf16; T = 32768 is level 0's first stack, 512 level 2's last): forward
     bit-identical to the unfused path; backward (dx and all four weight gradients, through the persistent
-    grid and the partial-row reduction at full size) against the unfused backward within the bf16 bound."""
+    grid and the partial-row reduction at full size) against fp64 autograd of the block on the same bf16 inputs
+    (the GPU's relu(h) masks; bf16 kernels) within 1e-2 relative L2 — the bf16 roundings of dh and dx — and
+    against the unfused HIP backward within the bf16 bound."""
     B = 32
     p = _block(B, T, d, seed=11 + d, dt=torch.bfloat16, cuda=cuda)
     h0, y0 = _unfused_fwd(p, d)
     h1, y1 = _fused_fwd(p, d)
     assert torch.equal(y1, y0)
     dx, g = _fused_bwd(p, d)
+    want = block_grads_fp64(p["x"], p["dy"], h1, bf16_weights(p), d)
+    errs = {"dx": _l2(dx, want[0])}
+    errs.update({k: _l2(g[k], gr) for k, gr in zip(("wa", "ba", "wb", "bb"), want[1:])})
+    print(f"T={T} d={d} fp64 relative L2: " + ", ".join(f"{k} {e:.2e}" for k, e in errs.items()))
+    for k, e in errs.items():
+        assert e < 1e-2, f"{k} vs fp64: {e:.3e}"
     dx0, ref = _unfused_bwd(p, d, h0)
     assert _l2(dx, dx0) < 2e-2
     for k in ref:

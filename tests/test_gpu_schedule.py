@@ -1,0 +1,116 @@
+"""Keras LearningRateSchedules in the product's Adam (vqa_optim.Adam + vqa_lr_schedule): the reference's
+transformer schedule CustomSchedule (src/transformer/multi_head_attention.py:82-101) and keras ExponentialDecay,
+evaluated on the device from the optimizer's step counter.
+
+Checks: the device rate equals the host (TF float32) evaluation at every step; each Adam update equals
+keras_adam (oracle, fp64) run with that step's rate (OptimizerV2._decayed_lr evaluates the schedule at
+iterations, before the increment: CustomSchedule's first rate is 0); a hipGraph-captured update replays the
+schedule (the rate changes from replay to replay) bitwise equal to eager updates; a scheduled Prior.train_step
+(Prior.compile(Adam(CustomSchedule(width)))) replays bitwise equal to eager steps.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"), ROOT]
+
+from oracle.vqvae_ref import keras_adam  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _store(n=4099, seed=0):
+    from vqa_layers import ParamStore
+    st = ParamStore()
+    st.add("w", (n,), "uniform")
+    st.add("b", (7,), "zeros")
+    st.materialize(torch.device("cuda"), seed=seed)
+    return st
+
+
+@pytest.mark.parametrize("sched", ["custom", "exp", "exp_stair"])
+def test_scheduled_adam_matches_keras(cuda, sched):
+    from schedules import CustomSchedule, ExponentialDecay
+    from vqa_optim import Adam
+    s = {"custom": CustomSchedule(128, warmup_steps=4), "exp": ExponentialDecay(1e-3, 3, 0.5),
+         "exp_stair": ExponentialDecay(1e-3, 2, 0.5, staircase=True)}[sched]
+    st = _store()
+    opt = Adam(learning_rate=s)
+    opt.build(st)
+    g = torch.Generator().manual_seed(1)
+    w = st.flat.detach().cpu().double()
+    m = torch.zeros_like(w)
+    v = torch.zeros_like(w)
+    for t in range(1, 8):
+        grad = torch.randn(st.size, generator=g) * 1e-2
+        st.grad.copy_(grad.float().cuda())
+        lr_host = s(t - 1)
+        assert opt.current_learning_rate() == lr_host
+        opt.apply(st)
+        torch.cuda.synchronize()
+        assert float(opt._lr_dev.item()) == pytest.approx(lr_host, rel=2e-7, abs=0.0), (t, lr_host)
+        w, m, v = keras_adam(w, grad.float().double(), m, v, t, lr=float(opt._lr_dev.item()))
+        got = st.flat.detach().cpu().double()
+        assert bool(((got - w).abs() <= 1e-6 * (w.abs() + 1e-2)).all()), (t, float((got - w).abs().max()))
+        w = got  # continue from the device state (fp32 rounding does not accumulate into the comparison)
+    if sched == "custom":
+        assert s(0) == 0.0  # rsqrt(0) = inf, 0 * warmup^-1.5 = 0: the first update is zero
+
+
+def test_scheduled_adam_graph_replay_bitwise(cuda):
+    from schedules import CustomSchedule
+    from vqa_optim import Adam
+    grads = [torch.randn(4099 + 11) * 1e-2 for _ in range(5)]
+    a, b = _store(), _store()
+    oa, ob = Adam(CustomSchedule(64, warmup_steps=3)), Adam(CustomSchedule(64, warmup_steps=3))
+    oa.build(a)
+    ob.build(b)
+    for gr in grads:
+        a.grad.copy_(gr[:a.size].cuda())
+        oa.apply(a)
+    gbuf = torch.zeros_like(b.grad)
+    b.grad = gbuf
+    gph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    with torch.cuda.graph(gph, stream=s):
+        ob.apply(b)
+    for gr in grads:
+        gbuf.copy_(gr[:b.size].cuda())
+        gph.replay()
+    torch.cuda.synchronize()
+    assert int(ob.iterations.item()) == 5
+    assert torch.equal(a.flat, b.flat) and torch.equal(oa.m, ob.m) and torch.equal(oa.v, ob.v)
+
+
+def test_prior_scheduled_graph_replay_matches_eager(cuda):
+    from oracle import prior_ref as P
+    from prior import Prior
+    from schedules import CustomSchedule
+    from vqa_optim import Adam
+    cfg = P.PriorConfig(bins=64, ctx=256, width=128, depth=2, heads=2, blocks=4, attn_stacks=1)
+
+    def make():
+        pr = Prior(0, [(cfg.ctx,)], cfg.bins, [3], [2], None,
+                   dict(width=cfg.width, depth=cfg.depth, heads=cfg.heads, blocks=cfg.blocks,
+                        attn_stacks=cfg.attn_stacks, drop_out_rate=0.1), None, dtype="fp32", device="cuda", seed=3)
+        pr.compile(optimizer=Adam(CustomSchedule(cfg.width, warmup_steps=2)))
+        return pr
+    codes = [torch.randint(0, cfg.bins - 1, (2, cfg.ctx), generator=torch.Generator().manual_seed(i)).cuda()
+             for i in range(4)]
+    a, b = make(), make()
+    for c in codes:
+        a.train_step(c)
+    b.capture_train_step(codes[0], warmup=1)
+    for c in codes[1:]:
+        b.train_step(c)
+    torch.cuda.synchronize()
+    assert torch.equal(a.prior.store.flat, b.prior.store.flat)
+    assert float(a.results()["loss"]) == float(b.results()["loss"])
+    lrs = [CustomSchedule(cfg.width, warmup_steps=2)(t) for t in range(4)]
+    assert lrs[0] == 0.0 and len(set(lrs)) == 4  # the replays ran with four different rates

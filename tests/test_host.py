@@ -38,7 +38,8 @@ def test_parameter_structure_matches_oracle(cfg):
 def test_cfg2_parameter_count():
     """968,835 trainable parameters in 570 tensors at cfg2."""
     store = _product_store(CFG2)
-    assert store.size == 968835 and len(store.specs) == 570
+    assert store.count == 968835 and len(store.specs) == 570 and store.size >= store.count
+    assert all(off % 4 == 0 for off, _ in store.offsets.values())  # 16-byte aligned tensors
 
 
 def test_init_matches_oracle_bitwise():
@@ -132,3 +133,28 @@ def test_splitsongs_and_tile():
     t = VectorQuantizer._tile(vq, torch.arange(12.).reshape(3, 4))
     assert t.shape == (9, 4) and torch.equal(t[3:6], t[:3])
     assert VectorQuantizer._tile(vq, torch.zeros(10, 4)).shape == (10, 4)
+
+
+def test_lr_schedules_host_values():
+    """src/transformer/multi_head_attention.py:82-101 CustomSchedule in TF float32 arithmetic, and keras
+    ExponentialDecay; the device kernel's constants come from the same host rounding."""
+    from schedules import CustomSchedule, ExponentialDecay
+    s = CustomSchedule(128, warmup_steps=4000)
+    f32 = np.float32
+    for step in (1, 10, 3999, 4000, 4001, 100000):
+        want = f32(f32(1) / np.sqrt(f32(128))) * min(f32(1) / np.sqrt(f32(step)), f32(f32(step) * f32(4000 ** -1.5)))
+        assert s(step) == float(f32(want)), step
+    assert s(0) == 0.0
+    peak = max(s(t) for t in (3999, 4000, 4001))
+    assert abs(peak - 128 ** -0.5 * 4000 ** -0.5) < 1e-9
+    kind, p = s.device_spec()
+    assert kind == 1 and p[0] == float(f32(1) / np.sqrt(f32(128)))
+    e = ExponentialDecay(0.1, 10, 0.5, staircase=True)
+    assert e(9) == float(f32(0.1)) and e(10) == float(f32(0.05)) and e(25) == float(f32(0.025))
+    assert abs(ExponentialDecay(0.1, 10, 0.5)(5) - 0.1 * 0.5 ** 0.5) < 1e-8
+
+
+def test_adam_rejects_host_callables():
+    from vqa_optim import Adam
+    with pytest.raises(TypeError):
+        Adam(learning_rate=lambda step: 1e-3)

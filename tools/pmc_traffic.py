@@ -56,6 +56,14 @@ def main():
         if busy and grbm:
             res["mfma_busy_frac"] = round(sum(busy) / (sum(grbm) / 8 * 1024), 4)
             res["mfma_dispatches"] = len(busy)
+    # provenance: the library these counters were read from (bench.py compares it with the library it loads)
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "vae-based-music--deep-generative-models_amd", "libvqa.so")
+    res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
+    res["commit"] = os.environ.get("VQA_COMMIT")  # the git HEAD the tree was sent from (no .git on the GPU box)
+    import time
+    res["measured_utc"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 

@@ -544,6 +544,7 @@ struct EmbArgs {
   float scale, rate;
   unsigned long long seed;
   const int64_t* ctr;  // optional device step counter mixed into the seed (advances under graph replay)
+  long long off;       // global flat index of out[0] (data parallel: rank * N*T*W) — the dropout mask's key
 };
 
 __device__ __forceinline__ unsigned long long seed_at(unsigned long long seed, const int64_t* ctr) {
@@ -573,7 +574,7 @@ __global__ __launch_bounds__(256) void prior_embed_kernel(EmbArgs a) {
       const float ks = 1.0f / (1.0f - a.rate);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        v[i] = prior_uniform(seed, kEmbDropSalt, (uint64_t)(r * a.W + c + i), 0) >= a.rate ? v[i] * ks : 0.f;
+        v[i] = prior_uniform(seed, kEmbDropSalt, (uint64_t)(a.off + r * a.W + c + i), 0) >= a.rate ? v[i] * ks : 0.f;
     }
     if (a.xcond) v = v + ld4((const T*)a.xcond + r * a.W + c);
     st4((T*)a.out + r * a.W + c, v);
@@ -602,14 +603,15 @@ __global__ __launch_bounds__(256) void axpy_kernel(const T* x, const T* y, T* z,
   }
 }
 
-// keras Dropout(rate): x * (1 / (1 - rate)) where u >= rate, else 0 (the same mask on the gradient)
+// keras Dropout(rate): x * (1 / (1 - rate)) where u >= rate, else 0 (the same mask on the gradient); the mask
+// is keyed on the global flat index off + e (data parallel: each rank passes its shard's first index)
 template <class T>
 __global__ __launch_bounds__(256) void dropout_kernel(T* x, long long n, float rate, unsigned long long seed0,
-                                                     unsigned long long salt, const int64_t* ctr) {
+                                                     unsigned long long salt, long long off, const int64_t* ctr) {
   const float ks = 1.0f / (1.0f - rate);
   const unsigned long long seed = seed_at(seed0, ctr);
   for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256)
-    st(x + e, prior_uniform(seed, salt, (uint64_t)e, 0) >= rate ? ld(x + e) * ks : 0.f);
+    st(x + e, prior_uniform(seed, salt, (uint64_t)(off + e), 0) >= rate ? ld(x + e) * ks : 0.f);
 }
 
 __global__ __launch_bounds__(256) void scale_f32_kernel(float* x, long long n, float s) {
@@ -1539,7 +1541,7 @@ struct DecArgs {
   int64_t* tokens;        // (N, steps + 1)
   float* kc;              // (N, depth, T, 32) key cache
   float* vc;              // (N, depth, T, 32) value cache
-  int N, steps, T, depth, H, l, bins;
+  int N, steps, T, depth, H, l, bins, ldo;  // ldo: head weight row stride (>= bins, % 4 == 0)
   long long start;
   unsigned long long seed;
   float scale, emb_scale, eps;
@@ -1750,7 +1752,7 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
       __syncthreads();
     }
     // output head + Gumbel-max
-    dec_matvec(x, kDecW, a.hw, a.hb, scr, a.bins, bestv);  // scr holds the logits
+    dec_matvec(x, kDecW, a.hw, a.hb, scr, a.ldo, bestv);  // scr holds the logits (ldo >= bins columns)
     float bv = -INFINITY;
     int bi = 0;
     for (int v = tid; v < a.bins; v += 256) {
@@ -1975,11 +1977,13 @@ extern "C" int vqa_seqlin_wgrad(const void* x, int64_t ldx, const void* dy, int6
 
 extern "C" int vqa_prior_embed_fwd(const float* table, const float* pos, const int64_t* tokens, const float* ycond,
                                    const void* xcond, void* out, int N, int T, int W, int bins, float scale, float rate,
-                                   uint64_t seed, const int64_t* counter, int dtype, vqa_stream_t stream) {
+                                   uint64_t seed, int64_t elem_offset, const int64_t* counter, int dtype,
+                                   vqa_stream_t stream) {
   VQA_ARG(table && pos && tokens && out && N > 0 && T > 0 && W > 0 && W % 4 == 0 && bins > 0 && rate >= 0.f &&
-              rate < 1.f, "prior_embed_fwd: bad arguments");
+              rate < 1.f && elem_offset >= 0, "prior_embed_fwd: bad arguments");
   VQA_ARG(pr_dt(dtype), "prior_embed_fwd: unknown dtype %d", dtype);
-  EmbArgs a{table, pos, tokens, ycond, xcond, out, (long long)N * T, T, W, bins, scale, rate, seed, counter};
+  EmbArgs a{table, pos, tokens, ycond, xcond, out, (long long)N * T, T, W, bins, scale, rate, seed, counter,
+            (long long)elem_offset};
   const unsigned g = pr_grid(a.rows * (W / 4));
   if (dtype == VQA_BF16) hipLaunchKernelGGL(prior_embed_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(prior_embed_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, a);
@@ -2014,17 +2018,17 @@ extern "C" int vqa_axpy(const void* x, const void* y, void* z, int64_t n, int dt
   return VQA_OK;
 }
 
-extern "C" int vqa_dropout(void* x, int64_t n, float rate, uint64_t seed, uint64_t salt, const int64_t* counter,
-                           int dtype, vqa_stream_t stream) {
-  VQA_ARG(x && n > 0 && rate >= 0.f && rate < 1.f && pr_dt(dtype), "dropout: bad arguments");
+extern "C" int vqa_dropout(void* x, int64_t n, float rate, uint64_t seed, uint64_t salt, int64_t elem_offset,
+                           const int64_t* counter, int dtype, vqa_stream_t stream) {
+  VQA_ARG(x && n > 0 && rate >= 0.f && rate < 1.f && elem_offset >= 0 && pr_dt(dtype), "dropout: bad arguments");
   if (rate == 0.f) return VQA_OK;
   const unsigned g = pr_grid(n);
   if (dtype == VQA_BF16)
     hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, (bf16*)x, (long long)n, rate,
-                       (unsigned long long)seed, (unsigned long long)salt, counter);
+                       (unsigned long long)seed, (unsigned long long)salt, (long long)elem_offset, counter);
   else
     hipLaunchKernelGGL(dropout_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (float*)x, (long long)n,
-                       rate, (unsigned long long)seed, (unsigned long long)salt, counter);
+                       rate, (unsigned long long)seed, (unsigned long long)salt, (long long)elem_offset, counter);
   VQA_LAUNCHED("dropout_kernel");
   return VQA_OK;
 }
@@ -2210,10 +2214,12 @@ extern "C" int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const 
                                 const float* pos_embedding, const float* out_kernel, const float* out_bias,
                                 const float* ycond, const float* xcond, const int64_t* forced, float* logits,
                                 int64_t* tokens, void* cache, size_t cache_bytes, int N, int steps, int ctx, int width,
-                                int heads, int blocks, int bins, int64_t start, uint64_t seed, vqa_stream_t stream) {
+                                int heads, int blocks, int bins, int out_ld, int64_t start, uint64_t seed,
+                                vqa_stream_t stream) {
   VQA_ARG(layers && x_embedding && pos_embedding && out_kernel && out_bias && tokens && cache && N > 0 && steps > 0 &&
-              steps <= ctx && blocks > 0 && ctx % blocks == 0 && bins > 0 && bins <= 2048 && bins % 4 == 0,
-          "prior_decode: bad arguments");
+              steps <= ctx && blocks > 0 && ctx % blocks == 0 && bins > 0 && out_ld >= bins && out_ld % 4 == 0 &&
+              out_ld <= 2048,
+          "prior_decode: bad arguments (bins %d, out_ld %d)", bins, out_ld);
   VQA_REQUIRE(depth > 0 && depth <= kDecMaxLayers && width == kDecW && heads > 0 && kDecAW % heads == 0 &&
                   kDecAW / heads <= 32 && ctx / blocks <= kDecMaxL && heads <= 4,
               VQA_E_UNSUPPORTED, "prior_decode: depth %d width %d heads %d block %d unsupported", depth, width, heads,
@@ -2235,7 +2241,7 @@ extern "C" int vqa_prior_decode(const vqa_prior_layer* layers, int depth, const 
   a.ycond = ycond; a.xcond = xcond; a.forced = forced; a.logits = logits; a.tokens = tokens;
   a.kc = (float*)cache;
   a.vc = (float*)cache + (size_t)N * depth * ctx * kDecAW;
-  a.N = N; a.steps = steps; a.T = ctx; a.depth = depth; a.H = heads; a.l = ctx / blocks; a.bins = bins;
+  a.N = N; a.steps = steps; a.T = ctx; a.depth = depth; a.H = heads; a.l = ctx / blocks; a.bins = bins; a.ldo = out_ld;
   a.start = start; a.seed = seed;
   a.scale = 1.0f / sqrtf((float)(kDecAW / heads));
   a.emb_scale = sqrtf((float)width);

@@ -46,8 +46,9 @@ __global__ __launch_bounds__(256) void mse_reduce_kernel(const float* ws, int n,
 // TF ApplyAdam (training_ops.cc, non-nesterov): alpha = lr*sqrt(1-b2^t)/(1-b1^t);
 // m += (g - m)*(1-b1); v += (g*g - v)*(1-b2); var -= (m*alpha)/(sqrt(v) + eps).
 __global__ __launch_bounds__(256) void adam_kernel(float* w, const float* g, float* m, float* v, long long n,
-                                                  const int64_t* step, float lr, float b1, float b2, float eps,
-                                                  float gs) {
+                                                  const int64_t* step, float lr0, const float* lr_dev, float b1,
+                                                  float b2, float eps, float gs) {
+  const float lr = lr_dev ? lr_dev[0] : lr0;  // a LearningRateSchedule's value at this step (vqa_lr_schedule)
   const float t = (float)(step[0] + 1);
   const float b1p = powf(b1, t), b2p = powf(b2, t);
   const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
@@ -61,6 +62,27 @@ __global__ __launch_bounds__(256) void adam_kernel(float* w, const float* g, flo
     v[i] = vi;
     w[i] = w[i] - (mi * alpha) / (sqrtf(vi) + eps);
   }
+}
+
+// keras LearningRateSchedule evaluated on the device at the optimizer's step counter (OptimizerV2._decayed_lr
+// calls the schedule with float(iterations), the count BEFORE this step's increment), so a captured step replays
+// with the right rate. Host-precomputed float32 constants keep the arithmetic TF's:
+//   kind 1  CustomSchedule (src/transformer/multi_head_attention.py:82-101): p0 = rsqrt(d_model),
+//           p1 = warmup_steps ** -1.5 -> p0 * min(rsqrt(s), s * p1)
+//   kind 2  keras ExponentialDecay: p0 = initial rate, p1 = decay_steps, p2 = decay_rate, p3 = staircase (0 / 1)
+//           -> p0 * p2 ** (s / p1), the exponent floored when staircase
+__global__ void lr_schedule_kernel(const int64_t* step, float* lr, int kind, float p0, float p1, float p2, float p3) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const float s = (float)step[0];
+  float r = p0;
+  if (kind == 1) {
+    r = p0 * fminf(1.0f / sqrtf(s), s * p1);
+  } else if (kind == 2) {
+    float e = s / p1;
+    if (p3 != 0.f) e = floorf(e);
+    r = p0 * powf(p2, e);
+  }
+  lr[0] = r;
 }
 
 __global__ void counter_add_kernel(int64_t* c, int64_t delta) {
@@ -158,11 +180,21 @@ extern "C" int vqa_mse_loss(const float* x, const float* r, const float* extra_g
 }
 
 extern "C" int vqa_adam_keras(float* w, const float* g, float* m, float* v, int64_t n, const int64_t* step, float lr,
-                              float beta1, float beta2, float eps, float grad_scale, vqa_stream_t stream) {
+                              const float* lr_dev, float beta1, float beta2, float eps, float grad_scale,
+                              vqa_stream_t stream) {
   VQA_ARG(w && g && m && v && step && n > 0, "adam: bad arguments");
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n, 4096)), dim3(256), 0, (hipStream_t)stream, w, g, m, v,
-                     (long long)n, step, lr, beta1, beta2, eps, grad_scale);
+                     (long long)n, step, lr, lr_dev, beta1, beta2, eps, grad_scale);
   VQA_LAUNCHED("adam_kernel");
+  return VQA_OK;
+}
+
+extern "C" int vqa_lr_schedule(const int64_t* step, float* lr, int kind, float p0, float p1, float p2, float p3,
+                               vqa_stream_t stream) {
+  VQA_ARG(step && lr && kind >= 0 && kind <= 2, "lr_schedule: bad arguments (kind %d)", kind);
+  VQA_ARG(kind != 2 || p1 > 0.f, "lr_schedule: decay_steps must be > 0");
+  hipLaunchKernelGGL(lr_schedule_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, lr, kind, p0, p1, p2, p3);
+  VQA_LAUNCHED("lr_schedule_kernel");
   return VQA_OK;
 }
 

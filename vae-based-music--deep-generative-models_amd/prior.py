@@ -130,8 +130,10 @@ class ResidualAttnBlock:
         return out
 
     # -------------------------------------------------------------- forward / backward on the device
-    def forward(self, x, T, training, save, seed, salt, counter=None):
-        """x (N, T, d) -> (N, T, d). save: keep what backward needs (layer input, qkv, heads, lse, o32, x1)."""
+    def forward(self, x, T, training, save, seed, salt, counter=None, row0=0):
+        """x (N, T, d) -> (N, T, d). save: keep what backward needs (layer input, qkv, heads, lse, o32, x1).
+        row0: the global index of x's first (sequence, position) row — the dropout mask's key under data
+        parallelism (rank * N * T), so every rank draws its slice of the single-process mask."""
         f, cdt, eps = self.fmha, x.dtype, 1e-6
         N = x.shape[0]
         w = f.width
@@ -161,7 +163,7 @@ class ResidualAttnBlock:
         drop = training and f.rate > 0
         if drop:
             V.seqlin_fwd_prepped(o32, wp["proj"], f.p("proj/bias"), x1, T)
-            V.dropout_(x1, f.rate, seed, salt, counter)
+            V.dropout_(x1, f.rate, seed, salt, counter, elem_offset=row0 * x.shape[-1])
             V.axpy(x1, x, x1)
         else:
             V.seqlin_fwd_prepped(o32, wp["proj"], f.p("proj/bias"), x1, T, residual=x)
@@ -174,12 +176,12 @@ class ResidualAttnBlock:
             h2 = torch.empty_like(x)
             V.layernorm_fwd(x1, g2, b2, h2, eps)
             V.seqlin_fwd_prepped(h2, wp["mlp"], self.store.view(f"{self.prefix}/mlp/bias"), out, T, residual=x1)
-        self._saved = (x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter) if save else None
+        self._saved = (x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter, row0) if save else None
         return out
 
     def backward(self, dout, T, deferred, post_adds):
         """dout = dL/d(out) -> dL/dx; weight gradients into the store (deferred partial reductions)."""
-        x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter = self._saved
+        x, qkv, qh, kh, vh, oh, lse, o32, x1, drop, seed, salt, counter, row0 = self._saved
         self._saved = None
         f, st, pre, eps = self.fmha, self.store, self.prefix, 1e-6
         N, w, cdt = x.shape[0], f.width, x.dtype
@@ -199,7 +201,7 @@ class ResidualAttnBlock:
         dres1 = dx1
         if drop:
             dres1 = dx1.clone()
-            V.dropout_(dres1, f.rate, seed, salt, counter)
+            V.dropout_(dres1, f.rate, seed, salt, counter, elem_offset=row0 * x.shape[-1])
         do32 = torch.empty_like(qh)
         V.seqlin_fwd_prepped(dres1, wp["proj_T"], None, do32, T)
         V.seqlin_wgrad(o32, dres1, f.g("proj/kernel"), f.g("proj/bias"), T, deferred=deferred)
@@ -332,11 +334,12 @@ class FMHABasedAutoregressiveModel:
         V.head_wt(self.store.view(self.out_kernel), wt)
         return wt
 
-    def _embed(self, tokens, training, x_cond=None, y_cond=None, seed=0, counter=None):
+    def _embed(self, tokens, training, x_cond=None, y_cond=None, seed=0, counter=None, row0=0):
         N, T = tokens.shape
         x = torch.empty(N, T, self.d_model, dtype=self.cdt, device=self.device)
         V.prior_embed_fwd(self.store.view(self.emb_name), self._pos(), tokens, x, math.sqrt(self.d_model),
-                          ycond=y_cond, xcond=x_cond, rate=self.rate if training else 0.0, seed=seed, counter=counter)
+                          ycond=y_cond, xcond=x_cond, rate=self.rate if training else 0.0, seed=seed, counter=counter,
+                          elem_offset=row0 * self.d_model)
         return x
 
     def prep_weights(self, bwd=False):
@@ -348,17 +351,26 @@ class FMHABasedAutoregressiveModel:
         V.seqlin_prep(descs, self.cdt)
 
     def hidden(self, tokens, training=False, x_cond=None, y_cond=None, save=False, seed=0, counter=None,
-               prepped=False):
-        """Embedding + transformer: (N, T) tokens -> (N, T, d) final hidden state (the head's input)."""
+               prepped=False, row0=0):
+        """Embedding + transformer: (N, T) tokens -> (N, T, d) final hidden state (the head's input). row0: the
+        global index of the first (sequence, position) row (data parallel: rank * N * T) — the dropout masks' key."""
         if not prepped:
             self.prep_weights(bwd=False)
         tokens = tokens.contiguous()
-        T = tokens.shape[1]
+        N, T = tokens.shape
         if self.use_pos_embedding and T > self.context_length:
             raise ValueError(f"sequence of {T} > context length {self.context_length}")
-        x = self._embed(tokens, training, x_cond, y_cond, seed, counter)
+        # the embedding kernel reads x_cond[n, t] (n < N, t < T) and y_cond[n]: check before passing pointers
+        if x_cond is not None and (x_cond.dim() != 3 or x_cond.shape[0] != N or x_cond.shape[1] < T
+                                   or x_cond.shape[2] != self.d_model):
+            raise ValueError(f"x_cond shape {tuple(x_cond.shape)}: expected ({N}, >= {T}, {self.d_model})")
+        if x_cond is not None and x_cond.shape[1] != T:
+            x_cond = x_cond[:, :T].contiguous()
+        if y_cond is not None and tuple(y_cond.shape) != (N, self.d_model):
+            raise ValueError(f"y_cond shape {tuple(y_cond.shape)}: expected ({N}, {self.d_model})")
+        x = self._embed(tokens, training, x_cond, y_cond, seed, counter, row0)
         for i, ly in enumerate(self.transformer.layers):
-            x = ly.forward(x, T, training, save, seed, 1000 + i, counter)
+            x = ly.forward(x, T, training, save, seed, 1000 + i, counter, row0)
         return x
 
     def _cond(self, x_cond, save=False):
@@ -377,24 +389,33 @@ class FMHABasedAutoregressiveModel:
         with torch.no_grad():
             h = self.hidden(tokens, training, self._cond(x_cond), self._ycond(y_cond))
             N, T = tokens.shape
-            wt32 = torch.empty(self.bins, self.d_model, dtype=torch.float32, device=self.device)
-            V.head_wt(self.store.view(self.out_kernel), wt32)
+            # the vocabulary zero-padded to a multiple of 16 (the sequence-linear kernel's output tile)
+            Vp = -(-self.bins // 16) * 16
+            wt32 = torch.zeros(Vp, self.d_model, dtype=torch.float32, device=self.device)
+            V.head_wt(self.store.view(self.out_kernel), wt32[:self.bins])
             hf = h.float().contiguous()
-            logits = torch.empty(N, T, self.bins, dtype=torch.float32, device=self.device)
-            b = self.store.view(self.out_bias)
-            for v0 in range(0, self.bins, 128):
-                n = min(128, self.bins - v0)
-                if n % 16:
-                    raise ValueError("bins must be a multiple of 16 to materialise logits")
+            logits = torch.empty(N, T, Vp, dtype=torch.float32, device=self.device)
+            b = torch.zeros(Vp, dtype=torch.float32, device=self.device)
+            b[:self.bins] = self.store.view(self.out_bias)
+            for v0 in range(0, Vp, 128):
+                n = min(128, Vp - v0)
                 V.seqlin_fwd(hf, wt32[v0:v0 + n], b[v0:v0 + n], logits[..., v0:v0 + n], T, wtrans=True)
-        return logits, {}
+        return (logits[..., :self.bins].contiguous() if Vp != self.bins else logits), {}
 
     call = __call__
 
-    def _ycond(self, y_cond):
+    def _ycond(self, y_cond, n=None):
+        """(N, d_model) fp32 label embeddings for position 0 (label_conditioners.py:26-45 gives (N, 1, d_model));
+        n: the number of sequences it must cover (the kernels read one row per sequence)."""
         if y_cond is None:
             return None
-        return torch.as_tensor(y_cond, device=self.device, dtype=torch.float32).reshape(-1, self.d_model).contiguous()
+        yc = torch.as_tensor(y_cond, device=self.device, dtype=torch.float32)
+        if yc.shape[-1] != self.d_model or yc.numel() % self.d_model:
+            raise ValueError(f"y_cond shape {tuple(yc.shape)}: last dimension must be {self.d_model}")
+        yc = yc.reshape(-1, self.d_model).contiguous()
+        if n is not None and yc.shape[0] != n:
+            raise ValueError(f"y_cond has {yc.shape[0]} rows for {n} sequences")
+        return yc
 
     def decode_cache(self, n_samples):
         nbytes = V.lib().vqa_prior_decode_cache_bytes(n_samples, self.depth, self.context_length)
@@ -405,25 +426,42 @@ class FMHABasedAutoregressiveModel:
         """autoregressive_fmha.py:162-240: (N, max_length + 1) int64 tokens starting with the start token, each
         next token = argmax(logits + Gumbel noise). One persistent decode launch."""
         L = self.context_length if max_length is None else int(max_length)
+        if not 0 < L <= self.context_length:
+            raise ValueError(f"max_length {L} outside (0, {self.context_length}]")
         xc = None
         if x_cond is not None:
+            # autoregressive_fmha.py:145-148 asserts x_cond is [n_samples, max_length, d_model] before adding it:
+            # the decode kernel reads x_cond[n, i] for every sample n and position i < L
             xc = self._cond(x_cond).float().contiguous()
-            if xc.shape[:2] != (n_samples, self.context_length) and xc.shape[1] < L:
-                raise ValueError(f"x_cond shape {tuple(xc.shape)} does not cover {L} positions")
+            if xc.dim() != 3 or xc.shape[0] != n_samples or xc.shape[1] < L or xc.shape[2] != self.d_model:
+                raise ValueError(f"x_cond shape {tuple(xc.shape)}: expected ({n_samples}, >= {L}, {self.d_model})")
             if xc.shape[1] != self.context_length:
                 full = torch.zeros(n_samples, self.context_length, self.d_model, device=self.device)
-                full[:, :xc.shape[1]] = xc
+                n = min(xc.shape[1], self.context_length)
+                full[:, :n] = xc[:, :n]
                 xc = full
         tokens = torch.empty(n_samples, L + 1, dtype=torch.int64, device=self.device)
         logits = (torch.empty(n_samples, L, self.bins, dtype=torch.float32, device=self.device)
                   if return_logits else None)
         if forced is not None:
             forced = torch.as_tensor(forced, device=self.device).long().contiguous()
+            if tuple(forced.shape) != (n_samples, L + 1):
+                raise ValueError(f"forced shape {tuple(forced.shape)}: expected ({n_samples}, {L + 1})")
+        yc = self._ycond(y_cond, n_samples)
         layers = [ly.layer_desc() for ly in self.transformer.layers]
-        V.prior_decode(layers, self.store.view(self.emb_name), self._pos().contiguous(),
-                       self.store.view(self.out_kernel), self.store.view(self.out_bias), tokens,
+        ow, ob = self.store.view(self.out_kernel), self.store.view(self.out_bias)
+        if self.bins % 4:
+            # the decode kernel's head mat-vec takes 16-byte column chunks: zero-pad the vocabulary to a multiple
+            # of 4 (the sampler's default 513 bins); the padded columns are never sampled
+            ld = -(-self.bins // 4) * 4
+            owp = torch.zeros(self.d_model, ld, device=self.device)
+            owp[:, :self.bins] = ow
+            obp = torch.zeros(ld, device=self.device)
+            obp[:self.bins] = ob
+            ow, ob = owp, obp
+        V.prior_decode(layers, self.store.view(self.emb_name), self._pos().contiguous(), ow, ob, tokens,
                        self.decode_cache(n_samples), L, self.context_length, self.heads, self.blocks,
-                       self.start_token, seed, ycond=self._ycond(y_cond), xcond=xc, forced=forced, logits=logits)
+                       self.start_token, seed, ycond=yc, xcond=xc, forced=forced, logits=logits, bins=self.bins)
         if return_logits:
             return tokens, logits
         if return_attention_weights:
@@ -530,6 +568,15 @@ class Prior:
     def metrics(self):
         return [self.train_loss_tracker, self.train_accuracy_tracker]
 
+    def compile(self, optimizer=None, **kwargs):
+        """keras Model.compile (the reference compiles with tf.keras.optimizers.Adam(), prior.py:436): a
+        vqa_optim.Adam whose learning_rate is a float or a LearningRateSchedule such as
+        schedules.CustomSchedule(d_model) (src/transformer/multi_head_attention.py:82-101), evaluated on the
+        device each step. A captured step is dropped (it holds the previous optimizer's buffers)."""
+        self.optimizer = optimizer or Adam()
+        self.optimizer.build(self.prior.store)
+        self._graph = None
+
     def reset_metrics(self):
         for m in self.metrics:
             m.reset_state()
@@ -612,7 +659,7 @@ class Prior:
         wt = m._wt(m.cdt)
         b = st.view(m.out_bias)
         with torch.no_grad():
-            h0 = m.hidden(latent, True, xc, yc, seed=seed * 7919 + 1, counter=ctr, prepped=True)
+            h0 = m.hidden(latent, True, xc, yc, seed=seed * 7919 + 1, counter=ctr, prepped=True, row0=row_offset)
             lse0 = torch.empty(M, dtype=torch.float32, device=dev)
             amax = torch.empty(N, T, dtype=torch.int64, device=dev)
             V.head_fwd(h0, wt, b, lse0, amax=amax)
@@ -622,7 +669,8 @@ class Prior:
         mask = None if tf_mask is None else torch.as_tensor(tf_mask, device=dev).to(torch.uint8).contiguous()
         V.tf_mix(codes, amax, mask, batch_input, m.start_token, rate=float(teacher_force_rate), seed=seed,
                  counter=ctr, row_offset=row_offset)
-        h = m.hidden(batch_input, True, xc, yc, save=True, seed=seed * 7919 + 2, counter=ctr, prepped=True)
+        h = m.hidden(batch_input, True, xc, yc, save=True, seed=seed * 7919 + 2, counter=ctr, prepped=True,
+                     row0=row_offset)
         lse = torch.empty(M, dtype=torch.float32, device=dev)
         loss_row = torch.empty(M, dtype=torch.float32, device=dev)
         correct = torch.empty(M, dtype=torch.float32, device=dev)
@@ -644,7 +692,7 @@ class Prior:
             if xc is not None:
                 m.conditioner.backward(dh)
             if m.rate > 0:  # the embedding dropout's mask, in place (dh is not read again)
-                V.dropout_(dh, m.rate, seed * 7919 + 2, V.EMB_DROPOUT_SALT, ctr)
+                V.dropout_(dh, m.rate, seed * 7919 + 2, V.EMB_DROPOUT_SALT, ctr, elem_offset=row_offset * m.d_model)
             if m.use_pos_embedding:
                 V.colsum(dh, st.grad_view(m.pos_name), N, T * m.d_model, T * m.d_model)
             gl = None
@@ -681,7 +729,9 @@ class Prior:
     def train_step(self, x, teacher_force_rate=0.2, tf_mask=None):
         """prior.py:241-335. tf_mask (N, T) bool overrides the random teacher-forcing draw (parity tests)."""
         codes, upper, y = self._codes(x)
-        if self._graph is not None and tf_mask is None and self._graph_fits(codes, upper, y):
+        # the captured graph bakes in its teacher-forcing rate: another rate (e.g. a schedule) runs eagerly
+        if (self._graph is not None and tf_mask is None and self._graph_fits(codes, upper, y)
+                and float(teacher_force_rate) == self._graph_rate):
             self._graph_in[0].copy_(codes)
             if upper is not None:
                 self._graph_in[1].copy_(upper)
@@ -706,7 +756,9 @@ class Prior:
         return same(codes, c) and same(upper, u) and same(y, l)
 
     def test_step(self, x):
-        """prior.py:337-372: loss / accuracy of the teacher-forced input (no mixing, no update)."""
+        """prior.py:337-372: loss / accuracy of the teacher-forced input (no mixing, no update). As in the
+        reference, the batch's values go into train_loss_tracker / train_accuracy_tracker and the running means
+        are returned (a keras evaluate loop over several batches reports their mean)."""
         m = self.prior
         codes, upper, y = self._codes(x)
         N, T = codes.shape
@@ -721,7 +773,9 @@ class Prior:
             out = torch.empty(2, dtype=torch.float32, device=self.device)
             V.rowsum(lr, 1, M, 1.0 / M, out[0:1])
             V.rowsum(cr, 1, M, 1.0 / M, out[1:2])
-        return {"loss": out[0], "perplexity(per word)": torch.exp(out[0]), "accuracy": out[1]}
+        self.train_loss_tracker.update_state(out[0])
+        self.train_accuracy_tracker.update_state(out[1])
+        return self.results()
 
     def capture_train_step(self, codes_example, teacher_force_rate=0.2, warmup=1):
         """Record the whole step (both passes, the conditioner, backward, Adam, metrics) as one hipGraph — two
@@ -752,6 +806,7 @@ class Prior:
             with torch.cuda.graph(g2, pool=pool):
                 self._apply()
         self._graph = (g1, g2)
+        self._graph_rate = float(teacher_force_rate)
         torch.cuda.synchronize(self.device)
 
     # -------------------------------------------------------------- checkpoint

@@ -20,12 +20,18 @@ import vqa_lib as V
 
 
 class ParamStore:
-    """Flat fp32 parameter / gradient storage with named views (Keras kernel layouts)."""
+    """Flat fp32 parameter / gradient storage with named views (Keras kernel layouts). Every tensor starts on a
+    16-byte boundary (offsets are multiples of 4 floats; the gaps stay zero, in the weights and the gradients),
+    so the kernels' 16-byte weight loads stay aligned whatever the sizes before it (a 513-bin head bias, a
+    1-channel output conv's bias)."""
+
+    ALIGN = 4  # floats
 
     def __init__(self):
         self.specs: List[Tuple[str, Tuple[int, ...], str]] = []  # (name, shape, init)
         self.offsets: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
-        self.size = 0
+        self.size = 0   # buffer length in floats (with the alignment gaps)
+        self.count = 0  # trainable values
         self.flat: Optional[torch.Tensor] = None
         self.grad: Optional[torch.Tensor] = None
         self.deferred = None  # a vqa_lib.Deferred while a model step batches its weight-gradient reductions
@@ -34,9 +40,11 @@ class ParamStore:
         if name in self.offsets:
             raise ValueError(f"duplicate parameter {name}")
         n = int(np.prod(shape))
-        self.offsets[name] = (self.size, tuple(shape))
+        off = -(-self.size // self.ALIGN) * self.ALIGN
+        self.offsets[name] = (off, tuple(shape))
         self.specs.append((name, tuple(shape), init))
-        self.size += n
+        self.size = off + n
+        self.count += n
         return name
 
     def init_values(self, seed: int = 1) -> Dict[str, np.ndarray]:
@@ -76,7 +84,7 @@ class ParamStore:
         return self.grad[off:off + int(np.prod(shape))].view(shape)
 
     def set_values(self, vals: Dict[str, np.ndarray]):
-        host = np.empty(self.size, np.float32)
+        host = np.zeros(self.size, np.float32)
         cur = self.flat.detach().cpu().numpy() if self.flat is not None else None
         for name, (off, shape) in self.offsets.items():
             n = int(np.prod(shape))

@@ -25,7 +25,7 @@ EXPORTED = [
     "vqa_conv1d_transpose_bwd_weight_workspace",
     "vqa_vq_sqnorm", "vqa_vq_argmin", "vqa_vq_quantize", "vqa_vq_quantize_workspace", "vqa_vq_backward",
     "vqa_vq_reset_rows", "vqa_vq_ema_apply", "vqa_reset_perm_index",
-    "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_counter_add",
+    "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_lr_schedule", "vqa_counter_add",
     "vqa_conv1d_bwd_weight_partials", "vqa_conv1d_transpose_bwd_weight_partials", "vqa_reduce_partials",
     "vqa_conv1d_bwd_data_weight", "vqa_conv1d_bwd_data_weight_workspace",
     "vqa_spectral_loss", "vqa_spectral_loss_workspace", "vqa_stft_magnitude",
@@ -81,7 +81,8 @@ _SIGS = {
     "vqa_reset_perm_index": (_L, [_U, _L, _I, _L, _L]),
     "vqa_mse_loss": (_I, [_P, _P, _P, _P, _P, _L, _P, _S, _P]),
     "vqa_mse_loss_workspace": (_S, [_L]),
-    "vqa_adam_keras": (_I, [_P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P]),
+    "vqa_adam_keras": (_I, [_P, _P, _P, _P, _L, _P, _F, _P, _F, _F, _F, _F, _P]),
+    "vqa_lr_schedule": (_I, [_P, _P, _I, _F, _F, _F, _F, _P]),
     "vqa_counter_add": (_I, [_P, _L, _P]),
     "vqa_step_metrics": (_I, [_P, _P, _P, _I, _F, _P]),
     "vqa_synthetic_batch": (_I, [_P, _I, _L, _U, _I, _F, _P]),
@@ -120,10 +121,10 @@ _SIGS = {
     "vqa_seqlin_fwd_ln_prepped": (_I, [_P, _L, _P, _P, ctypes.c_float, _P, _P, _P, _L, _P, _L] + [_I] * 7 + [_P]),
     "vqa_seqlin_wgrad_workspace": (_S, [_I] * 5),
     "vqa_seqlin_wgrad": (_I, [_P, _L, _P, _L, _P, _P] + [_I] * 6 + [_P, _S, _P, _P]),
-    "vqa_prior_embed_fwd": (_I, [_P] * 6 + [_I] * 4 + [_F, _F, _U, _P, _I, _P]),
+    "vqa_prior_embed_fwd": (_I, [_P] * 6 + [_I] * 4 + [_F, _F, _U, _L, _P, _I, _P]),
     "vqa_colsum": (_I, [_P, _P, _I, _L, _L, _I, _I, _P]),
     "vqa_axpy": (_I, [_P, _P, _P, _L, _I, _P]),
-    "vqa_dropout": (_I, [_P, _L, _F, _U, _U, _P, _I, _P]),
+    "vqa_dropout": (_I, [_P, _L, _F, _U, _U, _L, _P, _I, _P]),
     "vqa_scale_f32": (_I, [_P, _L, _F, _P]),
     "vqa_tf_mix": (_I, [_P, _P, _P, _P, _I, _I, _L, _F, _U, _U, _L, _P, _P]),
     "vqa_attn_fwd": (_I, [_P] * 6 + [_I] * 6 + [_F, _I, _P]),
@@ -135,7 +136,7 @@ _SIGS = {
     "vqa_rowsum_workspace": (_S, [_L, _L]),
     "vqa_rowsum": (_I, [_P, _L, _L, _F, _P, _P, _S, _P]),
     "vqa_prior_decode_cache_bytes": (_S, [_I, _I, _I]),
-    "vqa_prior_decode": (_I, [_P, _I] + [_P] * 10 + [_S] + [_I] * 7 + [_L, _U, _P]),
+    "vqa_prior_decode": (_I, [_P, _I] + [_P] * 10 + [_S] + [_I] * 8 + [_L, _U, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -413,9 +414,15 @@ def mse_loss(x, r, extra, dr, loss_out):
            "vqa_mse_loss")
 
 
-def adam_keras(w, g, m, v, step, lr, beta1, beta2, eps, grad_scale):
-    _check(lib().vqa_adam_keras(ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), ptr(step), lr, beta1, beta2, eps,
-                                grad_scale, stream()), "vqa_adam_keras")
+def adam_keras(w, g, m, v, step, lr, beta1, beta2, eps, grad_scale, lr_dev=None):
+    _check(lib().vqa_adam_keras(ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), ptr(step), float(lr), ptr(lr_dev), beta1,
+                                beta2, eps, grad_scale, stream()), "vqa_adam_keras")
+
+
+def lr_schedule(step, lr_out, kind, p):
+    p = list(p) + [0.0] * (4 - len(p))
+    _check(lib().vqa_lr_schedule(ptr(step), ptr(lr_out), int(kind), *[float(v) for v in p[:4]], stream()),
+           "vqa_lr_schedule")
 
 
 def step_metrics(loss_slots, vq_metrics, macc, levels, scale):
@@ -614,11 +621,13 @@ def seqlin_wgrad(x, dy, dw, db, T, taps=1, deferred=None):
         deferred.add(d, ws)
 
 
-def prior_embed_fwd(table, pos, tokens, out, scale, ycond=None, xcond=None, rate=0.0, seed=0, counter=None):
+def prior_embed_fwd(table, pos, tokens, out, scale, ycond=None, xcond=None, rate=0.0, seed=0, counter=None,
+                    elem_offset=0):
     N, T = tokens.shape
     bins, W = table.shape
     _check(lib().vqa_prior_embed_fwd(ptr(table), ptr(pos), ptr(tokens), ptr(ycond), ptr(xcond), ptr(out), N, T, W,
-                                     bins, scale, rate, seed, ptr(counter), dtype_code(out.dtype), stream()),
+                                     bins, scale, rate, seed, int(elem_offset), ptr(counter), dtype_code(out.dtype),
+                                     stream()),
            "vqa_prior_embed_fwd")
 
 
@@ -634,8 +643,10 @@ def axpy(x, y, z):
 EMB_DROPOUT_SALT = 0x454D42  # VQA_EMB_DROPOUT_SALT: vqa_prior_embed_fwd's dropout mask is vqa_dropout's with this salt
 
 
-def dropout_(x, rate, seed, salt, counter=None):
-    _check(lib().vqa_dropout(ptr(x), x.numel(), rate, seed, salt, ptr(counter), dtype_code(x.dtype), stream()),
+def dropout_(x, rate, seed, salt, counter=None, elem_offset=0):
+    """keras Dropout in place; elem_offset = the global flat index of x[0] (data parallel: rank * x.numel())."""
+    _check(lib().vqa_dropout(ptr(x), x.numel(), rate, seed, salt, int(elem_offset), ptr(counter), dtype_code(x.dtype),
+                             stream()),
            "vqa_dropout")
 
 
@@ -701,10 +712,12 @@ class PriorLayerDesc(ctypes.Structure):
 
 
 def prior_decode(layers, emb, pos, out_w, out_b, tokens, cache, steps, ctx, heads, blocks, start, seed, ycond=None,
-                 xcond=None, forced=None, logits=None):
+                 xcond=None, forced=None, logits=None, bins=None):
+    """out_w (width, ld) / out_b (ld,) with ld a multiple of 4 >= bins (zero-padded columns are never sampled)."""
     N = tokens.shape[0]
+    bins = out_w.shape[1] if bins is None else int(bins)
     arr = (PriorLayerDesc * len(layers))(*layers)
     _check(lib().vqa_prior_decode(arr, len(layers), ptr(emb), ptr(pos), ptr(out_w), ptr(out_b), ptr(ycond),
                                   ptr(xcond), ptr(forced), ptr(logits), ptr(tokens), ptr(cache), cache.numel(), N,
-                                  steps, ctx, emb.shape[1], heads, blocks, out_w.shape[1], start, seed, stream()),
+                                  steps, ctx, emb.shape[1], heads, blocks, bins, out_w.shape[1], start, seed, stream()),
            "vqa_prior_decode")
