@@ -17,6 +17,7 @@
 // per (item, resolution) and a third overlap-adds the frame gradients (fixed summation order:
 // deterministic) and applies the scales. No atomics, no host sync, graph-capturable.
 #include "vqa_common.h"
+#include <algorithm>
 
 namespace vqa {
 
@@ -227,11 +228,21 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
   }
 }
 
-// Frames in PAIRS (a, b) per slot: ONE complex FFT of z = w*s_a + i w*s_b gives both real frames' spectra
+// Frames in PAIRS (a, b): ONE complex FFT of z = w*s_a + i w*s_b gives both real frames' spectra
 // (S_a[k] = (Z[k] + conj Z[N-k]) / 2, S_b[k] = (Z[k] - conj Z[N-k]) / 2i). MAG writes |S| (the target's
 // spectrograms, once per step); LOSS / GRAD compare |S| of the reconstruction against the precomputed
 // target magnitudes and GRAD runs ONE inverse FFT of H_a + i H_b (both adjoint outputs are real, so
 // y_a = Re, y_b = Im). One FFT per frame (two with the gradient) instead of the three of a direct form.
+//
+// ONE WAVE PER FRAME PAIR (no workgroup barrier after the table load): each wave owns an LDS buffer of N
+// complex values and runs the Stockham FFT in it with register-resident radix-16 / 8 / 4 / 2 butterflies
+// (2048 = 16.16.8, 1024 = 16.16.4, 512 = 8.8.8, 256 = 16.16: three passes instead of the four to six of a
+// radix-8 / radix-4 plan). A pass loads every input of the lane's butterflies before it stores an output, and
+// all lanes of a wave execute each LDS instruction together (in order), so the passes run IN PLACE in one
+// buffer with no barrier between them. The first forward pass reads the windowed samples straight from HBM
+// (lane j of butterfly j takes samples j + r N/R: coalesced), the last inverse pass writes the windowed frame
+// gradients straight to HBM (samples q + S k: coalesced); the next pair's samples and target magnitudes are
+// prefetched into registers while the current pair is transformed.
 enum { PAIR_LOSS = 0, PAIR_GRAD = 1, PAIR_MAG = 2 };
 struct SpecPairArgs {
   const float* r;   // signal (B, T) fp32: reconstruction (LOSS, GRAD) or target (MAG)
@@ -243,76 +254,232 @@ struct SpecPairArgs {
   int B, T, F, hop, win;
 };
 
+// cos / sin (2 pi e / 16), e = 0..15 (the radix-16 butterfly's internal twiddles)
+__device__ constexpr float kC16[16] = {1.f, 0.92387953251128676f, 0.70710678118654752f, 0.38268343236508977f, 0.f,
+                                       -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128676f, -1.f,
+                                       -0.92387953251128676f, -0.70710678118654752f, -0.38268343236508977f, 0.f,
+                                       0.38268343236508977f, 0.70710678118654752f, 0.92387953251128676f};
+template <int E, bool INV> __device__ __forceinline__ f32x2 w16mul(f32x2 a) {
+  constexpr int e = E & 15;
+  if constexpr (e == 0) return a;
+  else if constexpr (e == 4) return INV ? f32x2{-a.y, a.x} : f32x2{a.y, -a.x};  // +-i
+  else if constexpr (e == 8) return f32x2{-a.x, -a.y};
+  else if constexpr (e == 12) return INV ? f32x2{a.y, -a.x} : f32x2{-a.y, a.x};
+  else {
+    const float c = kC16[e], sn = kC16[(e + 12) & 15];  // sin(2 pi e/16) = cos(2 pi (e - 4)/16)
+    const f32x2 w = INV ? f32x2{c, sn} : f32x2{c, -sn};
+    return cmul(a, w);
+  }
+}
+
+// X[k] = sum_r a[r] W_R^{rk} in place (W_R = exp(-+2 pi i / R)), natural order
+template <bool INV> __device__ __forceinline__ void dft4(f32x2& a0, f32x2& a1, f32x2& a2, f32x2& a3) {
+  const f32x2 b0 = a0 + a2, b1 = a0 - a2, b2 = a1 + a3, d = a1 - a3;
+  const f32x2 jd = INV ? f32x2{-d.y, d.x} : f32x2{d.y, -d.x};
+  a0 = b0 + b2;
+  a1 = b1 + jd;
+  a2 = b0 - b2;
+  a3 = b1 - jd;
+}
+template <int R, bool INV> __device__ __forceinline__ void dft(f32x2 (&a)[R]) {
+  if constexpr (R == 2) {
+    const f32x2 t = a[0] - a[1];
+    a[0] = a[0] + a[1];
+    a[1] = t;
+  } else if constexpr (R == 4) {
+    dft4<INV>(a[0], a[1], a[2], a[3]);
+  } else if constexpr (R == 8) {
+    // r = r1 + 2 r2 (r1 < 2, r2 < 4): 4-point DFTs over r2, W8^{r1 k2}, 2-point DFTs over r1
+    dft4<INV>(a[0], a[2], a[4], a[6]);
+    dft4<INV>(a[1], a[3], a[5], a[7]);
+    a[3] = w16mul<2, INV>(a[3]);
+    a[5] = w16mul<4, INV>(a[5]);
+    a[7] = w16mul<6, INV>(a[7]);
+    f32x2 o[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) {
+      o[k2] = a[2 * k2] + a[2 * k2 + 1];
+      o[k2 + 4] = a[2 * k2] - a[2 * k2 + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = o[k];
+  } else if constexpr (R == 16) {
+    // r = r1 + 4 r2: 4-point DFTs over r2 (B[r1][k2] lands in a[r1 + 4 k2]), W16^{r1 k2}, 4-point DFTs over r1
+#pragma unroll
+    for (int r1 = 0; r1 < 4; ++r1) dft4<INV>(a[r1], a[r1 + 4], a[r1 + 8], a[r1 + 12]);
+    a[5] = w16mul<1, INV>(a[5]);
+    a[9] = w16mul<2, INV>(a[9]);
+    a[13] = w16mul<3, INV>(a[13]);
+    a[6] = w16mul<2, INV>(a[6]);
+    a[10] = w16mul<4, INV>(a[10]);
+    a[14] = w16mul<6, INV>(a[14]);
+    a[7] = w16mul<3, INV>(a[7]);
+    a[11] = w16mul<6, INV>(a[11]);
+    a[15] = w16mul<9, INV>(a[15]);
+    f32x2 o[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) {
+      f32x2 c0 = a[4 * k2], c1 = a[4 * k2 + 1], c2 = a[4 * k2 + 2], c3 = a[4 * k2 + 3];
+      dft4<INV>(c0, c1, c2, c3);
+      o[k2] = c0;
+      o[k2 + 4] = c1;
+      o[k2 + 8] = c2;
+      o[k2 + 12] = c3;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = o[k];
+  }
+}
+
+// the radix plan of an N-point FFT: radix of pass s (0 when there is no such pass)
+template <int N, int P> constexpr int wradix() {
+  if constexpr (N == 2048) return P < 2 ? 16 : (P == 2 ? 8 : 0);
+  else if constexpr (N == 1024) return P < 2 ? 16 : (P == 2 ? 4 : 0);
+  else if constexpr (N == 512) return P < 3 ? 8 : 0;
+  else return P < 2 ? 16 : 0;  // 256
+}
+template <int N, int P> constexpr int wstride() { return P == 0 ? 1 : wstride<N, (P > 0 ? P - 1 : 0)>() * wradix<N, (P > 0 ? P - 1 : 0)>(); }
+
+constexpr int kSpecWaves = 4;  // waves (frame pairs in flight) per workgroup
+
+// the pass twiddles W_N^{k e}, k < R (conjugated for the inverse), from the fp64-rounded table; VQA_SPEC_TWD:
+// only k = 1, 2, 4, 8 from the table, the others one complex product away (fewer LDS reads, +1 ulp)
+template <int R, bool INV> __device__ __forceinline__ void pass_twiddles(f32x2 (&w)[R], const f32x2* tw, int e) {
+  w[0] = f32x2{1.f, 0.f};
+#ifdef VQA_SPEC_TWD
+#pragma unroll
+  for (int k = 1; k < R; k <<= 1) w[k] = tw[k * e];
+#pragma unroll
+  for (int k = 3; k < R; ++k)
+    if (k & (k - 1)) w[k] = cmul(w[k & -k], w[k - (k & -k)]);
+#else
+#pragma unroll
+  for (int k = 1; k < R; ++k) w[k] = tw[k * e];
+#endif
+  if (INV) {
+#pragma unroll
+    for (int k = 1; k < R; ++k) w[k] = conj2(w[k]);
+  }
+}
+
+// one Stockham pass of radix R at stride S over the wave's buffer z (in place): butterfly j = q + S p reads
+// z[q + S (p + r m)] and writes z[q + S (R p + k)] = W_N^{k p S} DFT_R(...)_k. Every load of the lane precedes
+// its first store (all lanes of the wave execute each LDS instruction together).
+template <int N, int R, int S, bool INV>
+__device__ __forceinline__ void wpass(f32x2* z, const f32x2* tw, int lane) {
+  constexpr int m = N / (S * R), NBF = N / R, IT = (NBF + 63) / 64;
+  f32x2 v[IT][R];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int j = lane + 64 * it;
+    if (NBF % 64 == 0 || j < NBF) {
+      const int p = j / S, q = j - p * S;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[it][r] = z[pidx(q + S * (p + r * m))];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int j = lane + 64 * it;
+    if (NBF % 64 == 0 || j < NBF) {
+      const int p = j / S, q = j - p * S;
+      dft<R, INV>(v[it]);
+      f32x2 w[R];
+      pass_twiddles<R, INV>(w, tw, p * S);
+#pragma unroll
+      for (int k = 0; k < R; ++k) z[pidx(q + S * (R * p + k))] = k ? cmul(v[it][k], w[k]) : v[it][k];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int N, int MODE>
-__global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
+__global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs a) {
   constexpr bool GRAD = MODE == PAIR_GRAD, MAG = MODE == PAIR_MAG;
-  constexpr int TPF = spec_tpf<N>(), FPI = 256 / TPF;  // frame-pair slots per workgroup
-  constexpr int KB = N / 2 + 1, NB = (KB + TPF - 1) / TPF, WPF = TPF / 64, NL = N / TPF;
+  constexpr int KB = N / 2 + 1, NB = (KB + 63) / 64;
+  constexpr int R0 = wradix<N, 0>(), R1 = wradix<N, 1>(), R2 = wradix<N, 2>();
+  constexpr int S1 = wstride<N, 1>(), S2 = wstride<N, 2>();
+  constexpr int NBF0 = N / R0, IT0 = (NBF0 + 63) / 64, M0 = N / R0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f32x2* tw = (f32x2*)smem;
   float* wn = (float*)(tw + N);
-  f32x2* slots = (f32x2*)(wn + ((a.win + 3) & ~3));
-  const int tid = threadIdx.x, sl = tid / TPF, lt = tid - sl * TPF, wave = tid >> 6;
-  f32x2* bA = slots + (size_t)sl * 2 * fpad<N>();
-  f32x2* bB = bA + fpad<N>();
-  __shared__ float red[4][4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x2* z = (f32x2*)(wn + N) + (size_t)wave * fpad<N>();
 
-  for (int e = tid; e < N / 2; e += 256) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
-  for (int e = tid; e < a.win; e += 256) wn[e] = a.wn[e];
+  // twiddles, and the window zero-padded to N (the FFT's zero padding without a per-sample branch)
+  for (int e = threadIdx.x; e < N / 2; e += 64 * kSpecWaves) ((float4*)tw)[e] = ((const float4*)a.tw)[e];
+  for (int e = threadIdx.x; e < N; e += 64 * kSpecWaves) wn[e] = e < a.win ? a.wn[e] : 0.f;
   __syncthreads();
 
   const int nframes = a.B * a.F, npairs = (nframes + 1) / 2;
-  // samples (and target magnitudes) of the slot's pair, loaded one pair ahead into registers
-  float ra[NL], rb[NL], ta[MAG ? 1 : NB], tb[MAG ? 1 : NB];
-  auto load_pair = [&](int p0) {
-    const int pa = min(2 * (p0 + sl), nframes - 1), pb = min(2 * (p0 + sl) + 1, nframes - 1);
-    const int ba_ = pa / a.F, bb_ = pb / a.F;
-    const size_t oa = (size_t)ba_ * a.T + (size_t)(pa - ba_ * a.F) * a.hop;
-    const size_t ob = (size_t)bb_ * a.T + (size_t)(pb - bb_ * a.F) * a.hop;
+  const int gw = blockIdx.x * kSpecWaves + wave, nw = gridDim.x * kSpecWaves;
+  // the pair's raw samples in pass-0 order (butterfly j = lane + 64 it, input r: sample j + r M0), loaded one
+  // pair ahead; its target magnitudes (bin lane + 64 j) are requested when the pair starts and land during its
+  // forward passes
+  float ra[IT0][R0], rb[IT0][R0], ta[MAG ? 1 : NB], tb[MAG ? 1 : NB];
+  auto frame_base = [&](int f) {
+    const int bb_ = f / a.F;
+    return a.r + (size_t)bb_ * a.T + (size_t)(f - bb_ * a.F) * a.hop;
+  };
+  auto load_samples = [&](int pp) {
+    const float* sa = frame_base(min(2 * pp, nframes - 1));
+    const float* sb = frame_base(min(2 * pp + 1, nframes - 1));
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int n = lt + i * TPF, nc = n < a.win ? n : 0;
-      ra[i] = a.r[oa + nc];
-      rb[i] = a.r[ob + nc];
-    }
+    for (int it = 0; it < IT0; ++it)
+#pragma unroll
+      for (int r = 0; r < R0; ++r) {
+        const int n = lane + 64 * it + r * M0, nc = n < a.win ? n : 0;
+        ra[it][r] = sa[nc];
+        rb[it][r] = sb[nc];
+      }
+  };
+  if (gw < npairs) load_samples(gw);
+  for (int pp = gw; pp < npairs; pp += nw) {
+    const int fa = 2 * pp, fb = fa + 1;
+    const bool acta = fa < nframes, actb = fb < nframes;
     if constexpr (!MAG) {
+      const int pa = min(fa, nframes - 1), pb = min(fb, nframes - 1);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const int k = lt + TPF * j, kc = k < KB ? k : 0;
+        const int k = lane + 64 * j, kc = k < KB ? k : 0;
         ta[j] = a.tm[(size_t)pa * KB + kc];
         tb[j] = a.tm[(size_t)pb * KB + kc];
       }
     }
-  };
-  if (blockIdx.x * FPI < npairs) load_pair(blockIdx.x * FPI);
-  for (int p0 = blockIdx.x * FPI; p0 < npairs; p0 += gridDim.x * FPI) {
-    const int fa = 2 * (p0 + sl), fb = fa + 1;
-    const bool acta = fa < nframes, actb = fb < nframes;
+    // pass 0 from the registers: windowed samples (n >= win: the FFT's zero padding), one butterfly at a time
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int n = lt + i * TPF;
-      bA[pidx(n)] = n < a.win ? f32x2{ra[i] * wn[n], rb[i] * wn[n]} : f32x2{0.f, 0.f};
-    }
-    float mxa[MAG ? 1 : NB], mxb[MAG ? 1 : NB];
-    if constexpr (!MAG) {
+    for (int it = 0; it < IT0; ++it) {
+      const int p = lane + 64 * it;  // S = 1: q = 0
+      if (NBF0 % 64 == 0 || p < NBF0) {
+        f32x2 v[R0];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        mxa[j] = ta[j];
-        mxb[j] = tb[j];
+        for (int r = 0; r < R0; ++r) {
+          const float w = wn[p + r * M0];
+          v[r] = f32x2{ra[it][r] * w, rb[it][r] * w};
+        }
+        dft<R0, false>(v);
+        f32x2 w[R0];
+        pass_twiddles<R0, false>(w, tw, p);
+#pragma unroll
+        for (int k = 0; k < R0; ++k) z[pidx(R0 * p + k)] = k ? cmul(v[k], w[k]) : v[k];
       }
     }
-    if (p0 + gridDim.x * FPI < npairs) load_pair(p0 + gridDim.x * FPI);  // lands during this pair's FFTs
-    __syncthreads();
-    f32x2* Z = fft<N, false, TPF>(bA, bB, tw, lt);
-    f32x2* sc = (Z == bA) ? bB : bA;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (pp + nw < npairs) load_samples(pp + nw);  // lands during this pair's remaining passes
+    wpass<N, R1, S1, false>(z, tw, lane);
+    if constexpr (R2 > 0) wpass<N, R2, S2, false>(z, tw, lane);
+    // bins: |S_a|, |S_b|, the loss partials and (GRAD) H = H_a + i H_b in place
     float sda = 0.f, sxa = 0.f, sdb = 0.f, sxb = 0.f;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int k = lt + TPF * j;
+      const int k = lane + 64 * j;
       if (k < KB) {
-        // bins k and N-k of Z are read and (GRAD) rewritten by this thread only: H is built in place
+        // bins k and N-k are read and (GRAD) rewritten by this lane only
         const int km = (N - k) & (N - 1);
-        const f32x2 zk = Z[pidx(k)], zm = Z[pidx(km)];
+        const f32x2 zk = z[pidx(k)], zm = z[pidx(km)];
         const f32x2 rka = f32x2{0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
         const f32x2 rkb = f32x2{0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x)};
         const float mra = cabs2(rka), mrb = cabs2(rkb);
@@ -320,22 +487,23 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
           if (acta) a.out[(size_t)fa * KB + k] = mra;
           if (actb) a.out[(size_t)fb * KB + k] = mrb;
         } else {
-          const float da = mxa[j] - mra, db = mxb[j] - mrb;
+          const float da = ta[j] - mra, db = tb[j] - mrb;
           sda += da * da;
-          sxa += mxa[j] * mxa[j];
+          sxa += ta[j] * ta[j];
           sdb += db * db;
-          sxb += mxb[j] * mxb[j];
+          sxb += tb[j] * tb[j];
           if constexpr (GRAD) {
-            // dL/d(Re,Im)R_k = (|R|-|X|) R/|R| (0 at |R| = 0); H = H_a + i H_b, each the Hermitian extension
-            // of G/2 (G at k = 0, N/2)
-            const float ga = mra > 0.f ? (mra - mxa[j]) / mra : 0.f;
-            const float gb = mrb > 0.f ? (mrb - mxb[j]) / mrb : 0.f;
+            // dL/d(Re,Im)R_k = (|R|-|X|) R/|R| (0 at |R| = 0); H = H_a + i H_b, each the Hermitian extension of
+            // G/2 (G at k = 0, N/2)
+            // 1/|R| by v_rcp_f32 (1 ulp): the gradient's tolerance is 1e-4 of its max, the loss does not use it
+            const float ga = mra > 0.f ? (mra - ta[j]) * __builtin_amdgcn_rcpf(mra) : 0.f;
+            const float gb = mrb > 0.f ? (mrb - tb[j]) * __builtin_amdgcn_rcpf(mrb) : 0.f;
             const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
             if (k == 0 || k == N / 2) {
-              Z[pidx(k)] = f32x2{Ga.x, Gb.x};
+              z[pidx(k)] = f32x2{Ga.x, Gb.x};
             } else {
-              Z[pidx(k)] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
-              Z[pidx(km)] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
+              z[pidx(k)] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
+              z[pidx(km)] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
             }
           }
         }
@@ -346,42 +514,54 @@ __global__ __launch_bounds__(256) void spec_pair_kernel(SpecPairArgs a) {
       sxa = warp_sum(sxa);
       sdb = warp_sum(sdb);
       sxb = warp_sum(sxb);
-      if ((tid & 63) == 0) {
-        red[0][wave] = sda;
-        red[1][wave] = sxa;
-        red[2][wave] = sdb;
-        red[3][wave] = sxb;
-      }
-    }
-    __syncthreads();  // also orders the H writes before the inverse FFT
-    if constexpr (!MAG) {
-      if (lt == 0) {
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int w = 0; w < WPF; ++w)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) s[v] += red[v][sl * WPF + w];
+      if (lane == 0) {
         if (acta) {
-          a.part[2 * (size_t)fa] = s[0];
-          a.part[2 * (size_t)fa + 1] = s[1];
+          a.part[2 * (size_t)fa] = sda;
+          a.part[2 * (size_t)fa + 1] = sxa;
         }
         if (actb) {
-          a.part[2 * (size_t)fb] = s[2];
-          a.part[2 * (size_t)fb + 1] = s[3];
+          a.part[2 * (size_t)fb] = sdb;
+          a.part[2 * (size_t)fb + 1] = sxb;
         }
       }
     }
     if constexpr (GRAD) {
-      const f32x2* Y = fft<N, true, TPF>(Z, sc, tw, lt);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // inverse FFT: passes 0 .. P-2 in LDS, the last pass straight to the frame gradients (windowed)
+      constexpr int RL = R2 > 0 ? R2 : R1, SL = R2 > 0 ? S2 : S1, NBFL = N / RL, ITL = (NBFL + 63) / 64;
+      wpass<N, R0, 1, true>(z, tw, lane);
+      if constexpr (R2 > 0) wpass<N, R1, S1, true>(z, tw, lane);
+      f32x2 v[ITL][RL];
+#pragma unroll
+      for (int it = 0; it < ITL; ++it) {
+        const int q = lane + 64 * it;  // the last pass: m = 1, p = 0, butterfly j = q < S
+        if (NBFL % 64 == 0 || q < NBFL) {
+#pragma unroll
+          for (int r = 0; r < RL; ++r) v[it][r] = z[pidx(q + SL * r)];
+        }
+      }
       float* oa = a.out + (size_t)fa * a.win;
       float* ob = a.out + (size_t)fb * a.win;
-      for (int n = lt; n < a.win; n += TPF) {
-        const f32x2 y = Y[pidx(n)];
-        if (acta) oa[n] = y.x * wn[n];
-        if (actb) ob[n] = y.y * wn[n];
+#pragma unroll
+      for (int it = 0; it < ITL; ++it) {
+        const int q = lane + 64 * it;
+        if (NBFL % 64 == 0 || q < NBFL) {
+          dft<RL, true>(v[it]);
+#pragma unroll
+          for (int k = 0; k < RL; ++k) {
+            const int n = q + SL * k;
+            if (n < a.win) {
+              if (acta) oa[n] = v[it][k].x * wn[n];
+              if (actb) ob[n] = v[it][k].y * wn[n];
+            }
+          }
+        }
       }
     }
-    __syncthreads();  // red[] and the slot buffers are reused by the next pair
+    // the next pair's pass 0 rewrites z: every read of it above precedes those stores in the wave's order
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -504,9 +684,8 @@ static int dispatch_frames(int n_fft, const SpecFrameArgs& fa, hipStream_t s) {
 
 template <int N, int MODE>
 static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
-  constexpr int FPI = 256 / spec_tpf<N>();
-  const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)((pa.win + 3) & ~3) * sizeof(float) +
-                     (size_t)FPI * 2 * fpad<N>() * sizeof(f32x2);
+  constexpr int FPI = kSpecWaves;  // frame pairs (one per wave) in flight per workgroup
+  const size_t lds = (size_t)N * sizeof(f32x2) + (size_t)N * sizeof(float) + (size_t)FPI * fpad<N>() * sizeof(f32x2);
   static size_t lds_set = 0;
   if (lds > 65536 && lds > lds_set) {
     if (hipFuncSetAttribute((const void*)spec_pair_kernel<N, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -517,10 +696,28 @@ static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
     }
     lds_set = lds;
   }
+  // persistent: as many workgroups as fit on the chip at once (LDS-bound), each wave walking its pairs with the
+  // next pair's samples prefetched; the tables are loaded once per workgroup
   const int npairs = (pa.B * pa.F + 1) / 2;
   const int groups = (npairs + FPI - 1) / FPI;
-  const int grid = groups < 2048 ? groups : 2048;
-  hipLaunchKernelGGL((spec_pair_kernel<N, MODE>), dim3(grid), dim3(256), lds, s, pa);
+  static int cus = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
+  }();
+  static size_t occ_lds = 0;  // resident workgroups per CU (LDS and registers), queried once per LDS size
+  static int per_cu = 1;
+  if (occ_lds != lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)spec_pair_kernel<N, MODE>, 64 * kSpecWaves,
+                                                     lds) != hipSuccess || per_cu <= 0) {
+      (void)hipGetLastError();
+      per_cu = 1;
+    }
+    occ_lds = lds;
+  }
+  const int grid = std::min(groups, cus * per_cu);
+  hipLaunchKernelGGL((spec_pair_kernel<N, MODE>), dim3(grid), dim3(64 * kSpecWaves), lds, s, pa);
   VQA_LAUNCHED("spec_pair_kernel");
   return VQA_OK;
 }
