@@ -748,6 +748,12 @@ template <class T> struct Chunk64 {
   }
 };
 
+// Ceiling (row attention at SMALL_PRIOR, B = 8, ctx 8192, 2 heads, blocks of 2048): 134 M causal scores, each
+// one v_exp_f32 (8 issue cycles per 64 lanes) plus ~4 other VALU (scale FMA, max, sum, bf16 pack) -> about
+// 20 us on 256 CUs; the QK / PV MFMAs (head dim 16, K = 16) are < 10 % of that. Measured 64 us (r2g/r3). A
+// single-wave-per-64-queries form without workgroup barriers (4 query groups per staged key tile) measured
+// 69.5 us: at 8 waves per CU the per-wave serial chain of the online softmax is not hidden, where this form
+// keeps 32 waves per CU.
 template <class T, int MODE>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   typedef Att<T> A;
