@@ -92,13 +92,24 @@ def multispectral_loss(target, recon):
     return torch.stack(losses, dim=-1).mean(dim=-1)
 
 
-def keras_adam(w, g, m, v, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
-    """TF ApplyAdam as used by keras 2.7 Adam; t is the 1-based step. Returns (w, m, v)."""
-    alpha = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+def keras_adam(w, g, m, v, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7, alpha=None):
+    """TF ApplyAdam as used by keras 2.7 Adam; t is the 1-based step. Returns (w, m, v). `alpha` overrides the
+    step size lr*sqrt(1-b2^t)/(1-b1^t) (e.g. with TF's float32 evaluation of the powers, adam_alpha_f32)."""
+    if alpha is None:
+        alpha = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
     m = m + (g - m) * (1 - b1)
     v = v + (g * g - v) * (1 - b2)
     w = w - (m * alpha) / (torch.sqrt(v) + eps)
     return w, m, v
+
+
+def adam_alpha_f32(lr, t, b1=0.9, b2=0.999):
+    """Keras Adam's step size as TF computes it: every hyper-parameter and beta^t in float32
+    (OptimizerV2 Adam._prepare_local: beta_2_power = pow(beta_2_t, local_step) in the variable dtype), so
+    1 - beta_2^t carries float32 cancellation at small t (~3e-5 relative at t = 2)."""
+    f = np.float32
+    b1p, b2p = f(f(b1) ** f(t)), f(f(b2) ** f(t))
+    return float(f(f(lr) * f(np.sqrt(f(f(1) - b2p)))) / f(f(1) - b1p))
 
 
 # ---------------------------------------------------------------------------------------------------

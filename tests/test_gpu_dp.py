@@ -17,8 +17,9 @@ Bounds (vs the single process on the global batch):
     <= 0.5 % of rows (fp32) / 2 % (bf16, where the fp32 master weights' last-bit differences also flip the
     bf16 rounding of a few weights), the number is printed; the EMA sums of every code whose count did not
     change L2 1e-3 / 2e-2; reset rows rel 2e-3 / 2e-2; weights within two Keras Adam updates
-    (|delta w| <= 2 lr) and relative L2 3e-3; with no row moved in fp32: weights / Adam moments / codebooks
-    rel 1e-5 and N_t bitwise;
+    (|delta w| <= 2 lr) and relative L2 3e-3; with no row moved in fp32: weights / Adam moments relative L2
+    1e-5 (an element with a pure-noise gradient still moves by +-lr: max |delta w| <= 2 lr), codebooks rel 1e-5
+    and N_t bitwise;
   always — the ranks' replicas are bitwise identical (weights, codebooks, EMA statistics).
 Also: bench.py itself under torchrun with 2 gloo ranks on the one GPU (the DP branch of the driver's
 command: split graphs around the exchange, max-over-ranks timing): one JSON line with value = 2 x
@@ -140,15 +141,26 @@ def _compare(r0, r1, s, K, D, L, phase, bf16):
         e, tol = _rel(r0["grads"] / 2, s["grads"]), (1e-5 if bf16 else 2e-6)
         check(e < tol, f"exchanged gradient rel {e:.2e} < {tol:g}")
     exact_path = phase == "step1" or (not bf16 and not any(flips.values()))
-    if exact_path:
+    if phase == "step1":
         # Adam normalises each element by sqrt(v): an element whose gradient nearly cancels across items keeps
         # its absolute rounding noise but has a small sqrt(v), so a 1e-7-relative gradient difference becomes
         # up to ~1e-3 of that element's update (lr = 1e-3 per step), i.e. a few 1e-6 of max|w|
         e = _rel(r0["weights"], s["weights"])
         check(e < 1e-5, f"weights rel {e:.2e} < 1e-5")
+        e = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"]))
+        check(e < 1e-5, f"Adam moments rel {e:.2e} < 1e-5")
+    elif exact_path:
+        # after the second update an element whose gradient is pure rounding noise (it cancels over the batch)
+        # has m / sqrt(v) = +-1 whatever its size, so the two runs can move it by +-lr in opposite directions
+        # (measured max |delta w| 1.3e-3 with no code moved): per element within two updates, and the whole
+        # tensor (L2) at fp32 rounding level
+        dw = float((r0["weights"] - s["weights"]).abs().max())
+        check(dw <= 2 * lr * 1.01, f"max |delta w| {dw:.2e} <= two Adam updates ({2 * lr:g})")
+        e = _l2(r0["weights"], s["weights"])
+        check(e < 1e-5, f"weights relative L2 {e:.2e} < 1e-5")
         if phase != "forward":
-            e = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"]))
-            check(e < 1e-5, f"Adam moments rel {e:.2e} < 1e-5")
+            e = max(_l2(r0["adam_m"], s["adam_m"]), _l2(r0["adam_v"], s["adam_v"]))
+            check(e < 1e-5, f"Adam moments relative L2 {e:.2e} < 1e-5")
     else:
         dw = float((r0["weights"] - s["weights"]).abs().max())
         check(dw <= 2 * lr * 1.01, f"max |delta w| {dw:.2e} <= two Adam updates ({2 * lr:g})")

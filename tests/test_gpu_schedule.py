@@ -18,7 +18,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"), ROOT]
 
-from oracle.vqvae_ref import keras_adam  # noqa: E402
+from oracle.vqvae_ref import adam_alpha_f32, keras_adam  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -53,11 +53,13 @@ def test_scheduled_adam_matches_keras(cuda, sched):
         opt.apply(st)
         torch.cuda.synchronize()
         assert float(opt._lr_dev.item()) == pytest.approx(lr_host, rel=2e-7, abs=0.0), (t, lr_host)
-        # TF's Adam holds beta_1, beta_2, epsilon as float32 hyper-parameters (the kernel's constants): with the
-        # large rates of a warm-up schedule the float32 beta_2 already moves alpha by ~1e-5 relative vs 0.999
+        # TF's Adam holds beta_1, beta_2, epsilon as float32 hyper-parameters (the kernel's constants) and
+        # evaluates beta^t and the step size in float32: at t = 2, 1 - beta_2^2 loses ~3e-5 relative to float32
+        # cancellation, which a warm-up schedule's large rate turns into ~1e-6 of a weight
         f32 = lambda c: float(np.float32(c))  # noqa: E731
-        w, m, v = keras_adam(w, grad.float().double(), m, v, t, lr=float(opt._lr_dev.item()), b1=f32(0.9),
-                             b2=f32(0.999), eps=f32(1e-7))
+        lr_t = float(opt._lr_dev.item())
+        w, m, v = keras_adam(w, grad.float().double(), m, v, t, lr=lr_t, b1=f32(0.9), b2=f32(0.999),
+                             eps=f32(1e-7), alpha=adam_alpha_f32(lr_t, t))
         got = st.flat.detach().cpu().double()
         assert bool(((got - w).abs() <= 1e-6 * (w.abs() + 1e-2)).all()), (t, float((got - w).abs().max()))
         w = got  # continue from the device state (fp32 rounding does not accumulate into the comparison)

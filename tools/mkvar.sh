@@ -1,0 +1,25 @@
+#!/bin/bash
+# Build a variant libvqa.so in which only the listed sources get extra compile flags (the other objects are the
+# product build's). Usage: tools/mkvar.sh NAME "EXTRA FLAGS" src1.hip [src2.hip ...]  ->  variants/NAME.so
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1; FLAGS=$2; shift 2
+C=vae-based-music--deep-generative-models_amd/csrc
+B=vae-based-music--deep-generative-models_amd/build
+VB=build_var_$NAME
+mkdir -p $VB variants
+make -s -C $C >/dev/null
+objs=""
+for o in $B/*.o; do
+  src=$(basename $o .o).hip
+  if [[ " $* " == *" $src "* ]]; then
+    /opt/rocm/bin/hipcc $FLAGS --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+      -Iinclude -mllvm -amdgpu-mfma-vgpr-form=1 -c $C/$src -o $VB/$(basename $o) &
+    objs="$objs $VB/$(basename $o)"
+  else
+    objs="$objs $o"
+  fi
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/$NAME.so $objs
+echo "variants/$NAME.so"

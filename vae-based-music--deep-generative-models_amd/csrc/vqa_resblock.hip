@@ -260,6 +260,21 @@ struct Rows32Buf {
   }
 };
 
+// (item, tile-in-item) of a workgroup's current tile, advanced without a division per tile
+struct RsCursor {
+  int n, tm;
+  __device__ __forceinline__ void set(int tile, int ntm) {
+    n = tile / ntm;
+    tm = tile - n * ntm;
+  }
+  __device__ __forceinline__ void next(int ntm) {
+    if (++tm == ntm) {
+      tm = 0;
+      ++n;
+    }
+  }
+};
+
 // chunks per thread for the largest tile of a launch (rows <= 256 at RMAXD)
 template <class T> constexpr int rs_pv() { return sizeof(T) == 2 ? 4 : 8; }
 
@@ -317,7 +332,8 @@ __device__ __forceinline__ void load_wfrags_t(typename Mfma<T>::frag (&wf)[3][2]
 // then channel blocks — the accumulation order of the unfused gather kernels.
 template <class T, bool RELU_IN, bool KPERM, bool ALDS, int NJ, class AFrag>
 __device__ __forceinline__ void conv_multi(f32x4 (&acc)[NJ][2], AFrag afrag, const T* in, const int (&rb)[NJ],
-                                           int tap_step) {
+                                           int tap_step, f32x4 init0 = f32x4{0.f, 0.f, 0.f, 0.f},
+                                           f32x4 init1 = f32x4{0.f, 0.f, 0.f, 0.f}) {
   typedef Mfma<T> M;
   constexpr int XS = rs_stride<T>(), NCC = rs_ncc<T>();
   const int lane = threadIdx.x & 63;
@@ -334,8 +350,8 @@ __device__ __forceinline__ void conv_multi(f32x4 (&acc)[NJ][2], AFrag afrag, con
       }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    acc[j][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[j][0] = init0;
+    acc[j][1] = init1;
   }
   typename M::frag af[3][NCC][2];
 #pragma unroll
@@ -368,6 +384,20 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o
 // 3 waves/SIMD for bf16 (<= 168 VGPRs without spilling); the fp32 parity build needs more registers
 // forward K order: natural (false) keeps it bit-identical to the unfused gather kernels
 constexpr bool kRsFwdKperm = false;
+// conv biases as the MFMA accumulators' initial values (no epilogue adds)
+#ifdef VQA_RS_BIASINIT
+constexpr bool kRsBiasInit = true;
+#else
+constexpr bool kRsBiasInit = false;
+#endif
+// bias-gradient MFMAs on every wave (the ct = 1 waves' sums are not stored): no wave-dependent branch
+#ifdef VQA_RS_BIASALL
+constexpr bool kRsBiasAll = true;
+#else
+constexpr bool kRsBiasAll = false;
+#endif
+__device__ __forceinline__ f32x4 rs_binit(f32x4 b) { return kRsBiasInit ? b : f32x4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ f32x4 rs_bepi(f32x4 acc, f32x4 b) { return kRsBiasInit ? acc : acc + b; }
 template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2; }
 
 // Rows per tile: chosen so that the recomputed rows fill whole 16-row MFMA tiles over the 4 waves
@@ -399,16 +429,23 @@ void resblock_fwd_kernel(ResArgs a) {
     bbv[mt] = a.bb ? bias4(a.bb, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
-  auto item_x = [&](int tile) { return rs_rsrc((const T*)a.x + (size_t)(tile / a.ntm) * a.T * RC, ibytes); };
-  auto row0 = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RT - 1 - d; };
+  auto load_x = [&](Rows32Buf<T, rs_pv<T>()>& bx, const RsCursor& c) {
+    bx.load(rs_rsrc((const T*)a.x + (size_t)c.n * a.T * RC, ibytes), c.tm * RT - 1 - d);
+  };
   Rows32Buf<T, rs_pv<T>()> nx;
   nx.init(XR, (XR + HR) * XS);  // trash row after H
-  nx.load(item_x(tbeg), row0(tbeg));
+  RsCursor cur, ldc;  // the tile being computed; the tile being loaded (cur + 1 or + 2)
+  cur.set(tbeg, a.ntm);
+  ldc = cur;
+  load_x(nx, ldc);
   nx.template store<false>(X);
-  if (tbeg + 1 < tend) nx.load(item_x(tbeg + 1), row0(tbeg + 1));
+  if (tbeg + 1 < tend) {
+    ldc.next(a.ntm);
+    load_x(nx, ldc);
+  }
   __syncthreads();
-  for (int tile = tbeg; tile < tend; ++tile) {
-    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RT;
+  for (int tile = tbeg; tile < tend; ++tile, cur.next(a.ntm)) {
+    const int n = cur.n, t0 = cur.tm * RT;
     // h rows t0-1 .. t0+RT+14 (conv_b reads t0-1 .. t0+RT); rows outside the item are conv_b's SAME zeros
     const bool interior = t0 - 1 >= 0 && t0 - 1 + HR <= a.T;  // uniform: no SAME-padding rows in h
     // y rows of this lane: n-tiles wave, wave+4, ... of RT/16; their residual x rows are read from X now, so
@@ -428,7 +465,7 @@ void resblock_fwd_kernel(ResArgs a) {
       f32x4 acc[3][2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = min(wave + 4 * j, HR / 16 - 1) * 16;
-      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d);
+      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d, rs_binit(bav[0]), rs_binit(bav[1]));
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= HR / 16) continue;
@@ -436,8 +473,8 @@ void resblock_fwd_kernel(ResArgs a) {
         const bool live = interior || (r >= 0 && r < a.T);
         if constexpr (sizeof(T) == 2) {
           // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8
-          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
-                                                                                            acc[j][1] + bav[1]))));
+          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(rs_bepi(acc[j][0], bav[0]),
+                                                                                            rs_bepi(acc[j][1], bav[1])))));
           if (!interior && !live) u = uint4{0u, 0u, 0u, 0u};
           *(uint4*)(H + i * XS + oc) = u;
           // the tile's own rows 1..RT (rows >= T dropped by the range check)
@@ -449,7 +486,7 @@ void resblock_fwd_kernel(ResArgs a) {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            v[mt] = acc[j][mt] + bav[mt];
+            v[mt] = rs_bepi(acc[j][mt], bav[mt]);
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
@@ -462,19 +499,22 @@ void resblock_fwd_kernel(ResArgs a) {
     __syncthreads();  // H complete; every read of X for this tile is done
     if (tile + 1 < tend) {
       nx.template store<false>(X);
-      if (tile + 2 < tend) nx.load(item_x(tile + 2), row0(tile + 2));
+      if (tile + 2 < tend) {
+        ldc.next(a.ntm);
+        load_x(nx, ldc);
+      }
     }
     {
       const __amdgpu_buffer_rsrc_t yr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
       f32x4 acc[NJ][2];
-      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1);
+      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1, rs_binit(bbv[0]), rs_binit(bbv[1]));
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (wave + 4 * j >= NT) continue;
         const int tl = ry[j] + pn;
         f32x4 x0, x1;
         xres[j].unpack(x0, x1);
-        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + (acc[j][0] + bbv[0]), x1 + (acc[j][1] + bbv[1]));
+        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + rs_bepi(acc[j][0], bbv[0]), x1 + rs_bepi(acc[j][1], bbv[1]));
       }
     }
     if (tile + 1 < tend) __syncthreads();  // every read of H done; the next tile's X is in LDS
@@ -519,23 +559,27 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   const int nht = HR / 16;  // <= 12
 
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
-  auto item_off = [&](int tile) { return (size_t)(tile / a.ntm) * a.T * RC; };
-  auto tstart = [&](int tile) { return (tile - (tile / a.ntm) * a.ntm) * RT; };
-  auto load_tile = [&](Rows32Buf<T, rs_pv<T>()>& bx, Rows32Buf<T, rs_pv<T>()>& by, int tile) {
-    const size_t o = item_off(tile);
-    bx.load(rs_rsrc((const T*)a.x + o, ibytes), tstart(tile) - 2 * d);
-    by.load(rs_rsrc((const T*)a.dy + o, ibytes), tstart(tile) - d - 1);
+  auto load_tile = [&](Rows32Buf<T, rs_pv<T>()>& bx, Rows32Buf<T, rs_pv<T>()>& by, const RsCursor& c) {
+    const size_t o = (size_t)c.n * a.T * RC;
+    bx.load(rs_rsrc((const T*)a.x + o, ibytes), c.tm * RT - 2 * d);
+    by.load(rs_rsrc((const T*)a.dy + o, ibytes), c.tm * RT - d - 1);
   };
   Rows32Buf<T, rs_pv<T>()> nx, ny;
   nx.init(XR, (XR + YR + HR) * XS);  // trash row after H
   ny.init(YR, (YR + HR) * XS);
-  load_tile(nx, ny, tbeg);
+  RsCursor cur, ldc;  // the tile being computed; the tile being loaded (cur + 1 or + 2)
+  cur.set(tbeg, a.ntm);
+  ldc = cur;
+  load_tile(nx, ny, ldc);
   nx.template store<true>(X);
   ny.template store<false>(Y);
-  if (tbeg + 1 < tend) load_tile(nx, ny, tbeg + 1);
+  if (tbeg + 1 < tend) {
+    ldc.next(a.ntm);
+    load_tile(nx, ny, ldc);
+  }
   __syncthreads();
-  for (int tile = tbeg; tile < tend; ++tile) {
-    const int n = tile / a.ntm, t0 = (tile - n * a.ntm) * RT;
+  for (int tile = tbeg; tile < tend; ++tile, cur.next(a.ntm)) {
+    const int n = cur.n, t0 = cur.tm * RT;
     // 1. recompute relu(h) over the dh rows (zero outside the item)
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
     int rh[3];
@@ -544,7 +588,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     if (!(a.skip & 1)) {
       f32x4 acc[3][2];
       auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
-      conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d);
+      conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d, rs_binit(bav[0]), rs_binit(bav[1]));
       if constexpr (sizeof(T) == 2) {
         // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8; the
         // SAME-padding rows of an edge tile are zeroed on a separate (wave-uniform) path
@@ -553,8 +597,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           for (int j = 0; j < 3; ++j) {
             if (wave + 4 * j >= nht) continue;
             const int i = rh[j] + pn;
-            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
-                                                                                              acc[j][1] + bav[1]))));
+            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(rs_bepi(acc[j][0], bav[0]),
+                                                                                              rs_bepi(acc[j][1], bav[1])))));
             if constexpr (decltype(edge)::value) {
               const int r = t0 - d + i;
               if (r < 0 || r >= a.T) u = uint4{0u, 0u, 0u, 0u};
@@ -574,7 +618,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            v[mt] = acc[j][mt] + bav[mt];
+            v[mt] = rs_bepi(acc[j][mt], bav[mt]);
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
@@ -594,7 +638,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           const typename M::frag af = rs_rows(H + (d + k - 1 + kk) * XS + ct * 16, XS);
           gwb[k] = M::mma(af, bf, gwb[k]);
         }
-        if (ct == 0) gbb = M::mma(M::ones(), bf, gbb);
+        if (kRsBiasAll || ct == 0) gbb = M::mma(M::ones(), bf, gbb);
       }
     }
     // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
@@ -632,7 +676,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     __syncthreads();
     // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows
     if (!(a.skip & 8)) {
-      const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + item_off(tile), ibytes);
+      const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
       int rb[NJ];
       f32x4 acc[NJ][2];
 #pragma unroll
@@ -664,14 +708,17 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           const typename M::frag af = rs_rows(X + ((k + 1) * d + kk) * XS + ct * 16, XS);
           gwa[k] = M::mma(af, bf, gwa[k]);
         }
-        if (ct == 0) gba = M::mma(M::ones(), bf, gba);
+        if (kRsBiasAll || ct == 0) gba = M::mma(M::ones(), bf, gba);
       }
     }
     if (tile + 1 < tend) {
       __syncthreads();  // every read of X, Y and H for this tile is done
       nx.template store<true>(X);
       ny.template store<false>(Y);
-      if (tile + 2 < tend) load_tile(nx, ny, tile + 2);
+      if (tile + 2 < tend) {
+        ldc.next(a.ntm);
+        load_tile(nx, ny, ldc);
+      }
       __syncthreads();
     }
   }
