@@ -21,4 +21,4 @@ for v in $OUT/base.so "$@"; do
 done
 cp $OUT/base.so $L
 paste $OUT/sw_base.txt $(for v in "$@"; do echo $OUT/sw_$(basename $v .so).txt; done) | sed 's/fused fwd//g' | cut -c1-250
-tools/ab_libs.sh 3 "$@"
+tools/ab_libs.sh ${ABR:-3} "$@"

@@ -214,7 +214,7 @@ constexpr int kRsOOB = -0x40000000;  // chunk offset that stays out of range for
 
 // Rows of a tile staged HBM -> registers -> LDS, 16 B per chunk. bf16 rows are 4 chunks; the 8 contiguous
 // lanes of one ds_write_b128 bank group take rows r and r + 4 (disjoint 16-dword windows at 80-byte rows).
-template <class T, int PV>
+template <class T, int PV, int NTH = 256>
 struct Rows32Buf {
   static constexpr int VEC = 16 / (int)sizeof(T), CPR = RC / VEC, ROWB = RC * (int)sizeof(T);
   uint4 v[PV];
@@ -225,7 +225,7 @@ struct Rows32Buf {
     constexpr int XS = RC + 16 / (int)sizeof(T);
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
-      const int e = threadIdx.x + i * 256;
+      const int e = threadIdx.x + i * NTH;
       int rr, q;
       if constexpr (CPR == 4) {
         const int G = e >> 3;
@@ -384,20 +384,7 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int o) { return f32x4{b[o
 // 3 waves/SIMD for bf16 (<= 168 VGPRs without spilling); the fp32 parity build needs more registers
 // forward K order: natural (false) keeps it bit-identical to the unfused gather kernels
 constexpr bool kRsFwdKperm = false;
-// conv biases as the MFMA accumulators' initial values (no epilogue adds)
-#ifdef VQA_RS_BIASINIT
-constexpr bool kRsBiasInit = true;
-#else
-constexpr bool kRsBiasInit = false;
-#endif
-// bias-gradient MFMAs on every wave (the ct = 1 waves' sums are not stored): no wave-dependent branch
-#ifdef VQA_RS_BIASALL
-constexpr bool kRsBiasAll = true;
-#else
-constexpr bool kRsBiasAll = false;
-#endif
-__device__ __forceinline__ f32x4 rs_binit(f32x4 b) { return kRsBiasInit ? b : f32x4{0.f, 0.f, 0.f, 0.f}; }
-__device__ __forceinline__ f32x4 rs_bepi(f32x4 acc, f32x4 b) { return kRsBiasInit ? acc : acc + b; }
+
 template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2; }
 
 // Rows per tile: chosen so that the recomputed rows fill whole 16-row MFMA tiles over the 4 waves
@@ -465,7 +452,7 @@ void resblock_fwd_kernel(ResArgs a) {
       f32x4 acc[3][2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = min(wave + 4 * j, HR / 16 - 1) * 16;
-      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d, rs_binit(bav[0]), rs_binit(bav[1]));
+      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= HR / 16) continue;
@@ -473,8 +460,8 @@ void resblock_fwd_kernel(ResArgs a) {
         const bool live = interior || (r >= 0 && r < a.T);
         if constexpr (sizeof(T) == 2) {
           // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8
-          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(rs_bepi(acc[j][0], bav[0]),
-                                                                                            rs_bepi(acc[j][1], bav[1])))));
+          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
+                                                                                            acc[j][1] + bav[1]))));
           if (!interior && !live) u = uint4{0u, 0u, 0u, 0u};
           *(uint4*)(H + i * XS + oc) = u;
           // the tile's own rows 1..RT (rows >= T dropped by the range check)
@@ -486,7 +473,7 @@ void resblock_fwd_kernel(ResArgs a) {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            v[mt] = rs_bepi(acc[j][mt], bav[mt]);
+            v[mt] = acc[j][mt] + bav[mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
@@ -507,14 +494,14 @@ void resblock_fwd_kernel(ResArgs a) {
     {
       const __amdgpu_buffer_rsrc_t yr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
       f32x4 acc[NJ][2];
-      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1, rs_binit(bbv[0]), rs_binit(bbv[1]));
+      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (wave + 4 * j >= NT) continue;
         const int tl = ry[j] + pn;
         f32x4 x0, x1;
         xres[j].unpack(x0, x1);
-        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + rs_bepi(acc[j][0], bbv[0]), x1 + rs_bepi(acc[j][1], bbv[1]));
+        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + (acc[j][0] + bbv[0]), x1 + (acc[j][1] + bbv[1]));
       }
     }
     if (tile + 1 < tend) __syncthreads();  // every read of H done; the next tile's X is in LDS
@@ -524,10 +511,17 @@ void resblock_fwd_kernel(ResArgs a) {
 // ---------------------------------------------------------------------------------------------------
 // DT > 0: the dilation as a compile-time constant (every LDS offset of the tile becomes an immediate);
 // DT = 0: any dilation <= RMAXD from the arguments
+// (an 8-wave variant — one workgroup per CU on 320-row tiles, the weight-gradient rows split over the two
+// 4-wave halves, one partial row per CU — measured equal per launch at T = 32768 and 0.3 ms/step slower
+// over the step: DESIGN.md §8)
 template <class T, int DT, int RT = rs_bwd_rt(DT)>
 __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
-  constexpr int WS = rs_stride<T>(), XS = WS, NT = RT / 16, NJ = (NT + 3) / 4;
+  constexpr int NW = 4;
+  constexpr int WS = rs_stride<T>(), XS = WS, NT = RT / 16, NJ = (NT + NW - 1) / NW;
+  constexpr int DM = DT > 0 ? DT : RMAXD, HRM = round16(RT + 2 * DM);
+  constexpr int PVX = ((HRM + 2 * DM) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
+  constexpr int PVY = ((HRM + 2) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int d = DT > 0 ? DT : a.d, HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
   // every weight operand lives in registers: conv_a's forward fragments (recompute h) and the two transposed
@@ -556,15 +550,17 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     gwa[k] = f32x4{0.f, 0.f, 0.f, 0.f};
     gwb[k] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int nht = HR / 16;  // <= 12
+  const int nht = HR / 16;  // <= 3 NW
+  static_assert(round16(RT + 2 * DM) / 16 <= 3 * NW, "recomputed rows: three 16-row tiles per wave");
 
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
-  auto load_tile = [&](Rows32Buf<T, rs_pv<T>()>& bx, Rows32Buf<T, rs_pv<T>()>& by, const RsCursor& c) {
+  auto load_tile = [&](Rows32Buf<T, PVX, 64 * NW>& bx, Rows32Buf<T, PVY, 64 * NW>& by, const RsCursor& c) {
     const size_t o = (size_t)c.n * a.T * RC;
     bx.load(rs_rsrc((const T*)a.x + o, ibytes), c.tm * RT - 2 * d);
     by.load(rs_rsrc((const T*)a.dy + o, ibytes), c.tm * RT - d - 1);
   };
-  Rows32Buf<T, rs_pv<T>()> nx, ny;
+  Rows32Buf<T, PVX, 64 * NW> nx;
+  Rows32Buf<T, PVY, 64 * NW> ny;
   nx.init(XR, (XR + YR + HR) * XS);  // trash row after H
   ny.init(YR, (YR + HR) * XS);
   RsCursor cur, ldc;  // the tile being computed; the tile being loaded (cur + 1 or + 2)
@@ -584,21 +580,21 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
     int rh[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) rh[j] = min(wave + 4 * j, nht - 1) * 16;
+    for (int j = 0; j < 3; ++j) rh[j] = min(wave + NW * j, nht - 1) * 16;
     if (!(a.skip & 1)) {
       f32x4 acc[3][2];
       auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
-      conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d, rs_binit(bav[0]), rs_binit(bav[1]));
+      conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d);
       if constexpr (sizeof(T) == 2) {
         // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8; the
         // SAME-padding rows of an edge tile are zeroed on a separate (wave-uniform) path
         auto store_h = [&](auto edge) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
-            if (wave + 4 * j >= nht) continue;
+            if (wave + NW * j >= nht) continue;
             const int i = rh[j] + pn;
-            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(rs_bepi(acc[j][0], bav[0]),
-                                                                                              rs_bepi(acc[j][1], bav[1])))));
+            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
+                                                                                              acc[j][1] + bav[1]))));
             if constexpr (decltype(edge)::value) {
               const int r = t0 - d + i;
               if (r < 0 || r >= a.T) u = uint4{0u, 0u, 0u, 0u};
@@ -611,14 +607,14 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       } else {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        if (wave + 4 * j >= nht) continue;
+        if (wave + NW * j >= nht) continue;
         const int i = rh[j] + pn, r = t0 - d + i;
         const bool live = interior || (r >= 0 && r < a.T);
         {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            v[mt] = rs_bepi(acc[j][mt], bav[mt]);
+            v[mt] = acc[j][mt] + bav[mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
@@ -638,7 +634,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           const typename M::frag af = rs_rows(H + (d + k - 1 + kk) * XS + ct * 16, XS);
           gwb[k] = M::mma(af, bf, gwb[k]);
         }
-        if (kRsBiasAll || ct == 0) gbb = M::mma(M::ones(), bf, gbb);
+        if (ct == 0) gbb = M::mma(M::ones(), bf, gbb);
       }
     }
     // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
@@ -668,7 +664,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     if (!(a.skip & 4)) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        if (wave + 4 * j >= nht) continue;
+        if (wave + NW * j >= nht) continue;
         if constexpr (sizeof(T) == 2) *(uint4*)(H + (rh[j] + pn) * XS + oc) = dhb[j];
         else st8(H + (rh[j] + pn) * XS + oc, dh[j][0], dh[j][1]);
       }
@@ -680,12 +676,12 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       int rb[NJ];
       f32x4 acc[NJ][2];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) rb[j] = min(wave + 4 * j, NT - 1) * 16 + 2 * d;
+      for (int j = 0; j < NJ; ++j) rb[j] = min(wave + NW * j, NT - 1) * 16 + 2 * d;
       conv_multi<T, false, true, false, NJ>(acc, [&](int k, int mt, int sc) { return wta[k][mt][sc]; }, H, rb, -d);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        if (wave + 4 * j >= NT) continue;
-        const int tl = (wave + 4 * j) * 16 + pn;
+        if (wave + NW * j >= NT) continue;
+        const int tl = (wave + NW * j) * 16 + pn;
         bool xp[8];
         f32x4 y0, y1;
         pos8(X + (tl + 2 * d) * XS + oc, xp);
@@ -708,7 +704,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           const typename M::frag af = rs_rows(X + ((k + 1) * d + kk) * XS + ct * 16, XS);
           gwa[k] = M::mma(af, bf, gwa[k]);
         }
-        if (kRsBiasAll || ct == 0) gba = M::mma(M::ones(), bf, gba);
+        if (ct == 0) gba = M::mma(M::ones(), bf, gba);
       }
     }
     if (tile + 1 < tend) {
@@ -788,6 +784,7 @@ template <class T> struct RsFwd {
 template <class T> struct RsBwd {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D>; }
 };
+
 template <class F> static const void* rs_pick(int d) {
   switch (d) {
     case 1: return F::template fn<1>();
