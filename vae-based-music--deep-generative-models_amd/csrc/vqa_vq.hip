@@ -140,7 +140,10 @@ __device__ __forceinline__ float vq_unpack_dist(unsigned long long p) {
 }
 
 // blockIdx.y = code split: codes [y*kspan, (y+1)*kspan); with more than one split the row results go to
-// idx as packed keys through atomicMin (vq_argmin_unpack_kernel turns them into indices / distances)
+// idx as packed keys through atomicMin (vq_argmin_unpack_kernel turns them into indices / distances).
+// Code chunks are double-buffered in LDS: the next chunk's global loads are in flight (registers) while the
+// current chunk runs its MFMAs, and land in the other buffer behind ONE barrier per chunk. Codes past the span
+// carry |e|^2 = +inf (their distance never wins), so the epilogue is add, fma, compare and two selects.
 template <int D>
 __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, const bf16* E3, const float* esq,
                                                              int64_t* idx, float* mind, long long N, int K,
@@ -150,8 +153,10 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
   constexpr int KC = kSplitKC, KS = D / 32, RT = 4;
   constexpr int CS = 3 * D + 8;          // LDS code stride (bf16): +16 B so 16 codes hit distinct banks
   constexpr int PPC = 3 * D * 2 / 16;    // 16-byte pieces per code
-  __shared__ __attribute__((aligned(16))) bf16 El[KC * CS];
-  __shared__ float el2[KC];
+  constexpr int NPT = KC * PPC / 256;    // pieces per thread per chunk
+  static_assert(KC * PPC % 256 == 0 && KC <= 256, "chunk staging");
+  __shared__ __attribute__((aligned(16))) bf16 El[2][KC * CS];
+  __shared__ float el2[2][KC];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long long n0 = (long long)blockIdx.x * 256 + wave * 64;
 
@@ -193,27 +198,43 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
       bidx[rt][r] = kbeg;  // no finite distance in this span: (inf, first code); the merge keeps code 0
     }
 
-  for (int k0 = kbeg; k0 < kend; k0 += KC) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < KC * PPC; e += 256) {
-      const int c = e / PPC, p = e - c * PPC;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (k0 + c < kend) v = *(const uint4*)(E3 + (size_t)(k0 + c) * 3 * D + p * 8);
-      *(uint4*)(El + c * CS + p * 8) = v;
+  // chunk staging: piece e = threadIdx.x + 256 p of code e / PPC
+  uint4 st[NPT];
+  float se2 = 0.f;
+  auto load_chunk = [&](int k0) {
+#pragma unroll
+    for (int p = 0; p < NPT; ++p) {
+      const int e = threadIdx.x + 256 * p, c = e / PPC, pc = e - c * PPC;
+      st[p] = k0 + c < kend ? *(const uint4*)(E3 + (size_t)(k0 + c) * 3 * D + pc * 8) : uint4{0u, 0u, 0u, 0u};
     }
-    for (int e = threadIdx.x; e < KC; e += 256) el2[e] = (k0 + e < kend) ? esq[k0 + e] : 0.f;
-    __syncthreads();
+    if (threadIdx.x < KC) se2 = k0 + (int)threadIdx.x < kend ? esq[k0 + threadIdx.x] : __builtin_inff();
+  };
+  auto store_chunk = [&](int b) {
+#pragma unroll
+    for (int p = 0; p < NPT; ++p) {
+      const int e = threadIdx.x + 256 * p, c = e / PPC, pc = e - c * PPC;
+      *(uint4*)(&El[b][c * CS + pc * 8]) = st[p];
+    }
+    if (threadIdx.x < KC) el2[b][threadIdx.x] = se2;
+  };
+  load_chunk(kbeg);
+  store_chunk(0);
+  __syncthreads();
+  int b = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += KC, b ^= 1) {
+    const bool more = k0 + KC < kend;
+    if (more) load_chunk(k0 + KC);  // lands while this chunk is compared
 #pragma unroll 1
     for (int ct = 0; ct < KC / 16; ++ct) {
       const int kl = ct * 16 + (lane & 15);
-      const bf16* eb = El + kl * CS + 8 * (lane >> 4);
+      const bf16* eb = &El[b][kl * CS + 8 * (lane >> 4)];
       bf16x8 bfr[3][KS];
 #pragma unroll
       for (int s = 0; s < 3; ++s)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) bfr[s][ks] = *(const bf16x8*)(eb + s * D + ks * 32);
       const int kg = k0 + kl;
-      const float e2 = el2[kl];
+      const float e2 = el2[b][kl];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -224,15 +245,17 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt][ks], bfr[s][ks], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float t = zq[rt][r] + e2;
-          const float dist = t - 2.0f * acc[r];
-          if (kg < kend && dist < best[rt][r]) {
+          // (|z|^2 + |e|^2) - 2 z.e as TF evaluates it: 2 z.e is exact, so the fma rounds once like the sub
+          const float dist = __builtin_fmaf(-2.0f, acc[r], zq[rt][r] + e2);
+          if (dist < best[rt][r]) {
             best[rt][r] = dist;
             bidx[rt][r] = kg;
           }
         }
       }
     }
+    if (more) store_chunk(b ^ 1);  // buffer b ^ 1 was last read before the previous barrier
+    __syncthreads();
   }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
