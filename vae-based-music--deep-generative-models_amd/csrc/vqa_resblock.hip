@@ -19,7 +19,6 @@
 // All products are MFMA (bf16 16x16x32 or the exact fp32 16x16x4 in parity mode), fp32 accumulation.
 #include "vqa_common.h"
 #include "vqa_mfma.h"
-#include <stdlib.h>
 #include <algorithm>
 #include <type_traits>
 
@@ -43,7 +42,6 @@ struct ResArgs {
   int B, T, d;
   int ntm, ntiles, tpw, textra;  // workgroup w owns tiles [w tpw + min(w, textra), +tpw + (w < textra))
   int nwg;
-  int skip;  // 0 in the product; -DVQA_RESBLOCK_ABLATION builds read VQA_RESBLOCK_SKIP (bit p skips phase p)
 };
 
 template <class T> constexpr int rs_stride() { return RC + lds_pad<T>(); }
@@ -509,61 +507,67 @@ void resblock_fwd_kernel(ResArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// DT > 0: the dilation as a compile-time constant (every LDS offset of the tile becomes an immediate);
-// DT = 0: any dilation <= RMAXD from the arguments
-// (an 8-wave variant — one workgroup per CU on 320-row tiles, the weight-gradient rows split over the two
-// 4-wave halves, one partial row per CU — measured equal per launch at T = 32768 and 0.3 ms/step slower
-// over the step: DESIGN.md §8)
+// Backward (h recomputed). DT > 0: the dilation as a compile-time constant (every LDS offset of the tile
+// becomes an immediate); DT = 0: any dilation <= RMAXD from the arguments. The work between two barriers is
+// split over two wave PAIRS ("teams"), so each weight gradient is accumulated by one pair over all 32 output
+// channels: every transposed K = rows fragment read for a weight-gradient product feeds 2 MFMAs instead of 1
+// (50 instead of 80 ds_read_b64_tr_b16 pairs per wave per tile), each wave holds two of the three
+// weight-fragment sets, and dh has an LDS buffer of its own (the single-team form with dh written over relu(h)
+// took 61.0 us where this takes 55.3, T = 32768, d = 9, bf16).
+//   all waves      h = relu(conv_a(relu x))            -> H                (rows t0-d .. t0+RT+d)
+//   team W (0, 1)  dW_b (input-channel tile = pair index, both output tiles) from H, Y;  then dx -> HBM
+//   team H (2, 3)  dh = conv_b^T(dy) * (h > 0) -> D (its own buffer);                then dW_a from X, D
+// Barriers per tile: H ready, D ready, every read done (then the next tile's staged rows are stored), the
+// stored rows visible: four (the one-buffer form needs five).
 template <class T, int DT, int RT = rs_bwd_rt(DT)>
 __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
   constexpr int NW = 4;
-  constexpr int WS = rs_stride<T>(), XS = WS, NT = RT / 16, NJ = (NT + NW - 1) / NW;
+  constexpr int XS = rs_stride<T>(), NT = RT / 16;
+  constexpr int NA = (NT + 1) / 2, NA1 = NA < 3 ? NA : 3, NA2 = NA - NA1;  // dx n-tiles per team-W wave
+  static_assert(NA2 >= 1 && NA2 <= 3, "dx: two batches per wave");
   constexpr int DM = DT > 0 ? DT : RMAXD, HRM = round16(RT + 2 * DM);
+  static_assert(HRM / 16 <= 12, "recomputed rows: 12 16-row tiles at most");
   constexpr int PVX = ((HRM + 2 * DM) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
   constexpr int PVY = ((HRM + 2) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int d = DT > 0 ? DT : a.d, HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
-  // every weight operand lives in registers: conv_a's forward fragments (recompute h) and the two transposed
-  // convs' fragments (dh, dx)
-  T* X = (T*)smem;              // local j <-> row t0 - 2d + j: relu(x)
-  T* Y = X + XR * XS;           // local m <-> row t0 - d - 1 + m (dy)
-  T* H = Y + YR * XS;           // local i <-> row t0 - d + i: relu(h), then dh
+  T* X = (T*)smem;     // local j <-> row t0 - 2d + j: relu(x)
+  T* Y = X + XR * XS;  // local m <-> row t0 - d - 1 + m (dy)
+  T* H = Y + YR * XS;  // local i <-> row t0 - d + i: relu(h)
+  T* D = H + HR * XS;  // local i <-> row t0 - d + i: dh
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int team = wave >> 1, tw = wave & 1;  // team 0 = W, 1 = H; tw = the pair's input-channel tile
   const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
             tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
-  typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()], wta[3][2][rs_ncc<T>()], wtb[3][2][rs_ncc<T>()];
+  // conv_a's forward fragments (recompute h) on every wave; team W: conv_a^T (dx), team H: conv_b^T (dh)
+  typename M::frag wfa[3][2][rs_ncc<T>()], wt[3][2][rs_ncc<T>()];
   load_wfrags<T, true>(wfa, a.wa);
-  load_wfrags_t<T>(wta, a.wa);
-  load_wfrags_t<T>(wtb, a.wb);
+  load_wfrags_t<T>(wt, team == 0 ? a.wa : a.wb);
   const int pn = rs_pi(lane & 15), oc = rs_ocol(lane);
   f32x4 bav[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) bav[mt] = a.ba ? bias4(a.ba, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // weight-gradient accumulators: wave w owns input-channel tile ct = w >> 1, output-channel tile ot = w & 1
-  const int ct = wave >> 1, ot = wave & 1;
-  f32x4 gwa[3], gwb[3], gba = {0.f, 0.f, 0.f, 0.f}, gbb = {0.f, 0.f, 0.f, 0.f};
+  // this pair's weight gradient: [output tile][tap] for input-channel tile tw, and the bias of output tile tw
+  f32x4 gw[2][3], gb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    gwa[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gwb[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int nht = HR / 16;  // <= 3 NW
-  static_assert(round16(RT + 2 * DM) / 16 <= 3 * NW, "recomputed rows: three 16-row tiles per wave");
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gw[o][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nht = HR / 16;
 
   const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
-  auto load_tile = [&](Rows32Buf<T, PVX, 64 * NW>& bx, Rows32Buf<T, PVY, 64 * NW>& by, const RsCursor& c) {
+  auto load_tile = [&](Rows32Buf<T, PVX>& bx, Rows32Buf<T, PVY>& by, const RsCursor& c) {
     const size_t o = (size_t)c.n * a.T * RC;
     bx.load(rs_rsrc((const T*)a.x + o, ibytes), c.tm * RT - 2 * d);
     by.load(rs_rsrc((const T*)a.dy + o, ibytes), c.tm * RT - d - 1);
   };
-  Rows32Buf<T, PVX, 64 * NW> nx;
-  Rows32Buf<T, PVY, 64 * NW> ny;
-  nx.init(XR, (XR + YR + HR) * XS);  // trash row after H
-  ny.init(YR, (YR + HR) * XS);
-  RsCursor cur, ldc;  // the tile being computed; the tile being loaded (cur + 1 or + 2)
+  Rows32Buf<T, PVX> nx;
+  Rows32Buf<T, PVY> ny;
+  nx.init(XR, (XR + YR + 2 * HR) * XS);  // trash row after D
+  ny.init(YR, (YR + 2 * HR) * XS);
+  RsCursor cur, ldc;
   cur.set(tbeg, a.ntm);
   ldc = cur;
   load_tile(nx, ny, ldc);
@@ -574,24 +578,24 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
     load_tile(nx, ny, ldc);
   }
   __syncthreads();
+  auto wt_frag = [&](int k, int mt, int sc) { return wt[k][mt][sc]; };
   for (int tile = tbeg; tile < tend; ++tile, cur.next(a.ntm)) {
     const int n = cur.n, t0 = cur.tm * RT;
-    // 1. recompute relu(h) over the dh rows (zero outside the item)
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
-    int rh[3];
+    // 1. relu(h) over the dh rows (zero outside the item): n-tiles wave, wave + 4, wave + 8
+    {
+      int rh[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) rh[j] = min(wave + NW * j, nht - 1) * 16;
-    if (!(a.skip & 1)) {
+      for (int j = 0; j < 3; ++j) rh[j] = min(wave + 4 * j, nht - 1) * 16;
       f32x4 acc[3][2];
-      auto wa_frag = [&](int k, int mt, int sc) { return wfa[k][mt][sc]; };
-      conv_multi<T, false, true, false, 3>(acc, wa_frag, X, rh, d);
+      conv_multi<T, false, true, false, 3>(acc, [&](int k, int mt, int sc) { return wfa[k][mt][sc]; }, X, rh, d);
       if constexpr (sizeof(T) == 2) {
         // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8; the
         // SAME-padding rows of an edge tile are zeroed on a separate (wave-uniform) path
         auto store_h = [&](auto edge) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
-            if (wave + NW * j >= nht) continue;
+            if (wave + 4 * j >= nht) continue;
             const int i = rh[j] + pn;
             uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
                                                                                               acc[j][1] + bav[1]))));
@@ -606,11 +610,10 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
         else store_h(std::true_type{});
       } else {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (wave + NW * j >= nht) continue;
-        const int i = rh[j] + pn, r = t0 - d + i;
-        const bool live = interior || (r >= 0 && r < a.T);
-        {
+        for (int j = 0; j < 3; ++j) {
+          if (wave + 4 * j >= nht) continue;
+          const int i = rh[j] + pn, r = t0 - d + i;
+          const bool live = interior || (r >= 0 && r < a.T);
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
@@ -621,94 +624,100 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           st8(H + i * XS + oc, v[0], v[1]);
         }
       }
-      }
     }
     __syncthreads();
-    // 2a. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o], db_b += sum_t dy[t] (the tile's own rows)
-    if (!(a.skip & 2)) {
+    if (team == 0) {
+      // 2W. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o] (c in tile tw, every o), db_b[o in tile tw]
 #pragma unroll
       for (int kk = 0; kk < RT; kk += M::KS) {
-        const typename M::frag bf = rs_rows(Y + (d + 1 + kk) * XS + ot * 16, XS);
+        const typename M::frag b0 = rs_rows(Y + (d + 1 + kk) * XS, XS);
+        const typename M::frag b1 = rs_rows(Y + (d + 1 + kk) * XS + 16, XS);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const typename M::frag af = rs_rows(H + (d + k - 1 + kk) * XS + ct * 16, XS);
-          gwb[k] = M::mma(af, bf, gwb[k]);
+          const typename M::frag af = rs_rows(H + (d + k - 1 + kk) * XS + tw * 16, XS);
+          gw[0][k] = M::mma(af, b0, gw[0][k]);
+          gw[1][k] = M::mma(af, b1, gw[1][k]);
         }
-        if (ct == 0) gbb = M::mma(M::ones(), bf, gbb);
+        gb = M::mma(M::ones(), tw ? b1 : b0, gb);
       }
-    }
-    // 2b. dh = conv_b^T(dy) * (h > 0), held in registers until every read of relu(h) is done
-    f32x4 dh[3][2];
-    uint4 dhb[3];  // bf16: the masked dh tile as raw bits (mask applied on the rounded values: same result)
-    if (!(a.skip & 4)) {
-      int rb[3];
+    } else {
+      // 2H. dh = conv_b^T(dy) * (h > 0) -> D: n-tiles tw, tw + 2, ..., in two batches of three
 #pragma unroll
-      for (int j = 0; j < 3; ++j) rb[j] = rh[j] + 2;
-      conv_multi<T, false, true, false, 3>(dh, [&](int k, int mt, int sc) { return wtb[k][mt][sc]; }, Y, rb, -1);
+      for (int q = 0; q < 2; ++q) {
+        int rh[3], rb[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if constexpr (sizeof(T) == 2) {
-          dhb[j] = mask_pos8(bf16_bits(dh[j][0], dh[j][1]), *(const uint4*)(H + (rh[j] + pn) * XS + oc));
-        } else {
-          bool hp[8];
-          pos8(H + (rh[j] + pn) * XS + oc, hp);
+        for (int j = 0; j < 3; ++j) {
+          rh[j] = min(tw + 2 * (3 * q + j), nht - 1) * 16;
+          rb[j] = rh[j] + 2;
+        }
+        f32x4 dh[3][2];
+        conv_multi<T, false, true, false, 3>(dh, wt_frag, Y, rb, -1);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            dh[j][0][q] = hp[q] ? dh[j][0][q] : 0.f;
-            dh[j][1][q] = hp[4 + q] ? dh[j][1][q] : 0.f;
+        for (int j = 0; j < 3; ++j) {
+          if (tw + 2 * (3 * q + j) >= nht) continue;
+          const int i = rh[j] + pn;
+          if constexpr (sizeof(T) == 2) {
+            // the mask on the rounded values: the same result as masking first
+            *(uint4*)(D + i * XS + oc) = mask_pos8(bf16_bits(dh[j][0], dh[j][1]), *(const uint4*)(H + i * XS + oc));
+          } else {
+            bool hp[8];
+            pos8(H + i * XS + oc, hp);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              dh[j][0][q] = hp[q] ? dh[j][0][q] : 0.f;
+              dh[j][1][q] = hp[4 + q] ? dh[j][1][q] : 0.f;
+            }
+            st8(D + i * XS + oc, dh[j][0], dh[j][1]);
           }
         }
       }
     }
     __syncthreads();
-    if (!(a.skip & 4)) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (wave + NW * j >= nht) continue;
-        if constexpr (sizeof(T) == 2) *(uint4*)(H + (rh[j] + pn) * XS + oc) = dhb[j];
-        else st8(H + (rh[j] + pn) * XS + oc, dh[j][0], dh[j][1]);
-      }
-    }
-    __syncthreads();
-    // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows
-    if (!(a.skip & 8)) {
+    if (team == 0) {
+      // 3W. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows: n-tiles tw, tw + 2, ... (NA per wave)
       const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
-      int rb[NJ];
-      f32x4 acc[NJ][2];
+      auto dx_batch = [&](auto nj, int j0) {
+        constexpr int NJB = decltype(nj)::value;
+        int rb[NJB];
+        f32x4 acc[NJB][2];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) rb[j] = min(wave + NW * j, NT - 1) * 16 + 2 * d;
-      conv_multi<T, false, true, false, NJ>(acc, [&](int k, int mt, int sc) { return wta[k][mt][sc]; }, H, rb, -d);
+        for (int j = 0; j < NJB; ++j) rb[j] = min(tw + 2 * (j0 + j), NT - 1) * 16 + 2 * d;
+        conv_multi<T, false, true, false, NJB>(acc, wt_frag, D, rb, -d);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if (wave + NW * j >= NT) continue;
-        const int tl = (wave + NW * j) * 16 + pn;
-        bool xp[8];
-        f32x4 y0, y1;
-        pos8(X + (tl + 2 * d) * XS + oc, xp);
-        ld8(Y + (tl + d + 1) * XS + oc, y0, y1);
+        for (int j = 0; j < NJB; ++j) {
+          if (tw + 2 * (j0 + j) >= NT) continue;
+          const int tl = (tw + 2 * (j0 + j)) * 16 + pn;
+          bool xp[8];
+          f32x4 y0, y1;
+          pos8(X + (tl + 2 * d) * XS + oc, xp);
+          ld8(Y + (tl + d + 1) * XS + oc, y0, y1);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          y0[q] += xp[q] ? acc[j][0][q] : 0.f;
-          y1[q] += xp[4 + q] ? acc[j][1][q] : 0.f;
+          for (int q = 0; q < 4; ++q) {
+            y0[q] += xp[q] ? acc[j][0][q] : 0.f;
+            y1[q] += xp[4 + q] ? acc[j][1][q] : 0.f;
+          }
+          st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
         }
-        st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
-      }
-    }
-    // 4. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o], db_a += sum_t dh[t]
-    if (!(a.skip & 16)) {
+      };
+      dx_batch(std::integral_constant<int, NA1>{}, 0);
+      dx_batch(std::integral_constant<int, NA2>{}, NA1);
+    } else {
+      // 4H. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o] (c in tile tw, every o), db_a[o in tile tw]
 #pragma unroll
       for (int kk = 0; kk < RT; kk += M::KS) {
-        const typename M::frag bf = rs_rows(H + (d + kk) * XS + ot * 16, XS);
+        const typename M::frag b0 = rs_rows(D + (d + kk) * XS, XS);
+        const typename M::frag b1 = rs_rows(D + (d + kk) * XS + 16, XS);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const typename M::frag af = rs_rows(X + ((k + 1) * d + kk) * XS + ct * 16, XS);
-          gwa[k] = M::mma(af, bf, gwa[k]);
+          const typename M::frag af = rs_rows(X + ((k + 1) * d + kk) * XS + tw * 16, XS);
+          gw[0][k] = M::mma(af, b0, gw[0][k]);
+          gw[1][k] = M::mma(af, b1, gw[1][k]);
         }
-        if (ct == 0) gba = M::mma(M::ones(), bf, gba);
+        gb = M::mma(M::ones(), tw ? b1 : b0, gb);
       }
     }
     if (tile + 1 < tend) {
-      __syncthreads();  // every read of X, Y and H for this tile is done
+      __syncthreads();  // every read of X, Y, H and D for this tile is done
       nx.template store<true>(X);
       ny.template store<false>(Y);
       if (tile + 2 < tend) {
@@ -718,22 +727,16 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       __syncthreads();
     }
   }
-  // partial rows: Keras dW[k][c][o] (c = ct*16 + 4*(lane>>4) + r, o = ot*16 + (lane&15)), then the bias
-  float* pa = a.part_a + (size_t)blockIdx.x * (3 * RC * RC + RC);
-  float* pb = a.part_b + (size_t)blockIdx.x * (3 * RC * RC + RC);
-  const int o = ot * 16 + (lane & 15);
+  // partial rows (team W: dW_b | db_b into part_b; team H: dW_a | db_a into part_a), Keras dW[k][c][o]
+  float* pr = (team == 0 ? a.part_b : a.part_a) + (size_t)blockIdx.x * (3 * RC * RC + RC);
 #pragma unroll
-  for (int k = 0; k < 3; ++k)
+  for (int o = 0; o < 2; ++o)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = ct * 16 + 4 * (lane >> 4) + r;
-      pa[(k * RC + c) * RC + o] = gwa[k][r];
-      pb[(k * RC + c) * RC + o] = gwb[k][r];
-    }
-  if (ct == 0 && lane < 16) {
-    pa[3 * RC * RC + o] = gba[0];
-    pb[3 * RC * RC + o] = gbb[0];
-  }
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pr[(k * RC + tw * 16 + 4 * (lane >> 4) + r) * RC + o * 16 + (lane & 15)] = gw[o][k][r];
+  if (lane < 16) pr[3 * RC * RC + tw * 16 + lane] = gb[0];
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -754,9 +757,10 @@ static size_t fwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = rt + 16;
   return ((size_t)(HR + 2 * d) * s + (size_t)HR * s + s) * esz;
 }
+// X (HR + 2d rows), Y (HR + 2), relu(h) and dh (HR each), the trash row
 static size_t bwd_lds(int d, int esz, int rt) {
   const int s = RC + 16 / esz, HR = round16(rt + 2 * d);
-  return ((size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)HR * s + s) * esz;
+  return ((size_t)(HR + 2 * d) * s + (size_t)(HR + 2) * s + (size_t)2 * HR * s + s) * esz;
 }
 
 static int set_lds(const void* fn, size_t bytes) {
@@ -784,6 +788,7 @@ template <class T> struct RsFwd {
 template <class T> struct RsBwd {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D>; }
 };
+
 
 template <class F> static const void* rs_pick(int d) {
   switch (d) {
@@ -826,7 +831,7 @@ extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba,
   VQA_REQUIRE(vqa_resblock_supported(C, dilation, dtype), VQA_E_UNSUPPORTED,
               "resblock_fwd: unsupported C=%d dilation=%d dtype=%d", C, dilation, dtype);
   VQA_ARG((long long)T * C * 4 < (1ll << 30), "resblock_fwd: item too long for 32-bit buffer offsets (T=%d)", T);
-  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0, 0, 0, 0};
+  ResArgs a{x, nullptr, y, h_out, wa, ba, wb, bb, nullptr, nullptr, B, T, dilation, 0, 0, 0, 0, 0};
   plan(a, 3, fwd_rt_of(dilation));
   const int esz = dtype == VQA_BF16 ? 2 : 4;
   // one LDS reservation for every dilation (the largest plan)
@@ -861,15 +866,7 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   const size_t need = vqa_resblock_bwd_workspace(B, T, C, dilation, dtype);
   VQA_ARG(workspace && ws_bytes >= need, "resblock_bwd: workspace %zu < %zu bytes", ws_bytes, need);
   const int E = 3 * RC * RC + RC;
-  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0, 0, 0};
-#ifdef VQA_RESBLOCK_ABLATION
-  // development builds only (make ABLATION=1, tools/ablate_res.sh): phases skipped, gradients WRONG
-  static const int dbg_skip = [] {
-    const char* e = getenv("VQA_RESBLOCK_SKIP");
-    return e ? atoi(e) : 0;
-  }();
-  a.skip = dbg_skip;
-#endif
+  ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0, 0};
   // at least kResMinTiles tiles per workgroup: a workgroup's weight-gradient partial row (2 x 3,104 fp32) is
   // larger than a tile's activations, so short launches use fewer, longer-lived workgroups
   plan(a, kResPerCU, bwd_rt_of(dilation), kResMinTiles);
