@@ -389,6 +389,8 @@ template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2;
 // (forward: RT + 16 = 192 = 12 tiles; backward: round16(RT + 2d) <= 192 with RT a multiple of 32 for the
 // K = rows weight-gradient products)
 constexpr int rs_fwd_rt(int dt) { return dt > 0 ? 176 : RTM; }
+// (192-row tiles for d <= 9 and 160 for d = 27 — fewer recomputed halo rows per output row — measured slower
+// on the step: 7.59 / 7.53 vs 7.51 ms)
 constexpr int rs_bwd_rt(int dt) { return (dt > 0 && dt <= 9) ? 160 : RTM; }
 
 template <class T, int DT, int RT = rs_fwd_rt(DT)>
@@ -524,10 +526,15 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
   constexpr int NW = 4;
   constexpr int XS = rs_stride<T>(), NT = RT / 16;
-  constexpr int NA = (NT + 1) / 2, NA1 = NA < 3 ? NA : 3, NA2 = NA - NA1;  // dx n-tiles per team-W wave
-  static_assert(NA2 >= 1 && NA2 <= 3, "dx: two batches per wave");
+  // dx n-tiles per team-W wave (interleaved), in batches NA1 + NA2 (a team-H share measured slower)
+  constexpr int NA = (NT + 1) / 2, NA1 = NA < 3 ? NA : 3, NA2 = NA - NA1;
+  static_assert(NA2 >= 1 && NA2 <= 3, "dx: two batches per team-W wave");
   constexpr int DM = DT > 0 ? DT : RMAXD, HRM = round16(RT + 2 * DM);
-  static_assert(HRM / 16 <= 12, "recomputed rows: 12 16-row tiles at most");
+  // recomputed 16-row tiles: NP1 per wave for h (batches P1A + P1B), NDH per team-H wave for dh (DH1 + DH2 + DH3)
+  constexpr int NHT = HRM / 16, NP1 = (NHT + 3) / 4, P1A = NP1 < 3 ? NP1 : 3, P1B = NP1 - P1A;
+  constexpr int NDH = (NHT + 1) / 2, DH1 = NDH < 3 ? NDH : 3, DH2 = NDH - DH1 < 3 ? NDH - DH1 : 3,
+                DH3 = NDH - DH1 - DH2;
+  static_assert(P1B <= 3 && DH3 <= 3, "recomputed rows: at most 24 16-row tiles");
   constexpr int PVX = ((HRM + 2 * DM) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
   constexpr int PVY = ((HRM + 2) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -582,20 +589,21 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   for (int tile = tbeg; tile < tend; ++tile, cur.next(a.ntm)) {
     const int n = cur.n, t0 = cur.tm * RT;
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
-    // 1. relu(h) over the dh rows (zero outside the item): n-tiles wave, wave + 4, wave + 8
-    {
-      int rh[3];
+    // 1. relu(h) over the dh rows (zero outside the item): n-tiles wave + 4 (j0 + j)
+    auto h_batch = [&](auto nj, int j0) {
+      constexpr int NJB = decltype(nj)::value;
+      int rh[NJB];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) rh[j] = min(wave + 4 * j, nht - 1) * 16;
-      f32x4 acc[3][2];
-      conv_multi<T, false, true, false, 3>(acc, [&](int k, int mt, int sc) { return wfa[k][mt][sc]; }, X, rh, d);
+      for (int j = 0; j < NJB; ++j) rh[j] = min(wave + 4 * (j0 + j), nht - 1) * 16;
+      f32x4 acc[NJB][2];
+      conv_multi<T, false, true, false, NJB>(acc, [&](int k, int mt, int sc) { return wfa[k][mt][sc]; }, X, rh, d);
       if constexpr (sizeof(T) == 2) {
         // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8; the
         // SAME-padding rows of an edge tile are zeroed on a separate (wave-uniform) path
         auto store_h = [&](auto edge) {
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            if (wave + 4 * j >= nht) continue;
+          for (int j = 0; j < NJB; ++j) {
+            if (wave + 4 * (j0 + j) >= nht) continue;
             const int i = rh[j] + pn;
             uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
                                                                                               acc[j][1] + bav[1]))));
@@ -610,8 +618,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
         else store_h(std::true_type{});
       } else {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (wave + 4 * j >= nht) continue;
+        for (int j = 0; j < NJB; ++j) {
+          if (wave + 4 * (j0 + j) >= nht) continue;
           const int i = rh[j] + pn, r = t0 - d + i;
           const bool live = interior || (r >= 0 && r < a.T);
           f32x4 v[2];
@@ -624,7 +632,9 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           st8(H + i * XS + oc, v[0], v[1]);
         }
       }
-    }
+    };
+    h_batch(std::integral_constant<int, P1A>{}, 0);
+    if constexpr (P1B > 0) h_batch(std::integral_constant<int, P1B>{}, P1A);
     __syncthreads();
     if (team == 0) {
       // 2W. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o] (c in tile tw, every o), db_b[o in tile tw]
@@ -641,20 +651,20 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
         gb = M::mma(M::ones(), tw ? b1 : b0, gb);
       }
     } else {
-      // 2H. dh = conv_b^T(dy) * (h > 0) -> D: n-tiles tw, tw + 2, ..., in two batches of three
+      // 2H. dh = conv_b^T(dy) * (h > 0) -> D: n-tiles tw + 2 (j0 + j)
+      auto dh_batch = [&](auto nj, int j0) {
+        constexpr int NJB = decltype(nj)::value;
+        int rh[NJB], rb[NJB];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        int rh[3], rb[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          rh[j] = min(tw + 2 * (3 * q + j), nht - 1) * 16;
+        for (int j = 0; j < NJB; ++j) {
+          rh[j] = min(tw + 2 * (j0 + j), nht - 1) * 16;
           rb[j] = rh[j] + 2;
         }
-        f32x4 dh[3][2];
-        conv_multi<T, false, true, false, 3>(dh, wt_frag, Y, rb, -1);
+        f32x4 dh[NJB][2];
+        conv_multi<T, false, true, false, NJB>(dh, wt_frag, Y, rb, -1);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (tw + 2 * (3 * q + j) >= nht) continue;
+        for (int j = 0; j < NJB; ++j) {
+          if (tw + 2 * (j0 + j) >= nht) continue;
           const int i = rh[j] + pn;
           if constexpr (sizeof(T) == 2) {
             // the mask on the rounded values: the same result as masking first
@@ -670,37 +680,41 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
             st8(D + i * XS + oc, dh[j][0], dh[j][1]);
           }
         }
-      }
+      };
+      dh_batch(std::integral_constant<int, DH1>{}, 0);
+      if constexpr (DH2 > 0) dh_batch(std::integral_constant<int, DH2>{}, DH1);
+      if constexpr (DH3 > 0) dh_batch(std::integral_constant<int, DH3>{}, DH1 + DH2);
     }
     __syncthreads();
-    if (team == 0) {
-      // 3W. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows: n-tiles tw, tw + 2, ... (NA per wave)
-      const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
-      auto dx_batch = [&](auto nj, int j0) {
-        constexpr int NJB = decltype(nj)::value;
-        int rb[NJB];
-        f32x4 acc[NJB][2];
+    // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows, NJB n-tiles nt(j) at a time (nt(j) >= NT: none)
+    const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
+    auto dx_batch = [&](auto nj, auto nt, auto frag) {
+      constexpr int NJB = decltype(nj)::value;
+      int rb[NJB];
+      f32x4 acc[NJB][2];
 #pragma unroll
-        for (int j = 0; j < NJB; ++j) rb[j] = min(tw + 2 * (j0 + j), NT - 1) * 16 + 2 * d;
-        conv_multi<T, false, true, false, NJB>(acc, wt_frag, D, rb, -d);
+      for (int j = 0; j < NJB; ++j) rb[j] = min(nt(j), NT - 1) * 16 + 2 * d;
+      conv_multi<T, false, true, false, NJB>(acc, frag, D, rb, -d);
 #pragma unroll
-        for (int j = 0; j < NJB; ++j) {
-          if (tw + 2 * (j0 + j) >= NT) continue;
-          const int tl = (tw + 2 * (j0 + j)) * 16 + pn;
-          bool xp[8];
-          f32x4 y0, y1;
-          pos8(X + (tl + 2 * d) * XS + oc, xp);
-          ld8(Y + (tl + d + 1) * XS + oc, y0, y1);
+      for (int j = 0; j < NJB; ++j) {
+        if (nt(j) >= NT) continue;
+        const int tl = nt(j) * 16 + pn;
+        bool xp[8];
+        f32x4 y0, y1;
+        pos8(X + (tl + 2 * d) * XS + oc, xp);
+        ld8(Y + (tl + d + 1) * XS + oc, y0, y1);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            y0[q] += xp[q] ? acc[j][0][q] : 0.f;
-            y1[q] += xp[4 + q] ? acc[j][1][q] : 0.f;
-          }
-          st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
+        for (int q = 0; q < 4; ++q) {
+          y0[q] += xp[q] ? acc[j][0][q] : 0.f;
+          y1[q] += xp[4 + q] ? acc[j][1][q] : 0.f;
         }
-      };
-      dx_batch(std::integral_constant<int, NA1>{}, 0);
-      dx_batch(std::integral_constant<int, NA2>{}, NA1);
+        st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
+      }
+    };
+    if (team == 0) {
+      // 3W. n-tiles tw, tw + 2, ...
+      dx_batch(std::integral_constant<int, NA1>{}, [&](int j) { return tw + 2 * j; }, wt_frag);
+      dx_batch(std::integral_constant<int, NA2>{}, [&](int j) { return tw + 2 * (NA1 + j); }, wt_frag);
     } else {
       // 4H. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o] (c in tile tw, every o), db_a[o in tile tw]
 #pragma unroll
@@ -874,7 +888,8 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   a.part_b = a.part_a + (size_t)nwg * E;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
   const size_t lds = bwd_lds(dilation, esz, bwd_rt_of(dilation));
-  const size_t lds_max = std::max(bwd_lds(RMAXD, esz, RTM), bwd_lds(9, esz, rs_bwd_rt(9)));
+  size_t lds_max = bwd_lds(RMAXD, esz, RTM);  // one reservation for every dilation (the largest plan)
+  for (int dd : {1, 3, 9, 27}) lds_max = std::max(lds_max, bwd_lds(dd, esz, rs_bwd_rt(dd)));
   const hipStream_t s = (hipStream_t)stream;
   const void* fn = dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation);
   if (int rc = set_lds(fn, lds_max)) return rc;
