@@ -52,7 +52,8 @@ def snapshot(m):
             "grads": m.bucket[:P].detach().cpu().clone(),
             "vq": [{k: torch.as_tensor(v) for k, v in st.items() if k != "calls"} | {"calls": st["calls"]}
                    for st in m.get_vq_state()],
-            "results": {k: float(v) for k, v in m.results().items()}}
+            "results": {k: float(v) for k, v in m.results().items()},
+            "offsets": {k: (int(o), int(torch.Size(sh).numel())) for k, (o, sh) in m.store.offsets.items()}}
 
 
 def run(m, xs, mode):

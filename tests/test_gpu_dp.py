@@ -139,7 +139,13 @@ def _compare(r0, r1, s, K, D, L, phase, bf16):
         # the exchanged gradient (sum over ranks of rank-mean gradients) = world x the global-batch mean
         # gradient, to fp32 rounding of the different summation grouping
         e, tol = _rel(r0["grads"] / 2, s["grads"]), (1e-5 if bf16 else 2e-6)
-        check(e < tol, f"exchanged gradient rel {e:.2e} < {tol:g}")
+        worst = ""
+        if e >= tol and "offsets" in s:  # which parameters differ (diagnostic)
+            gmax = float(s["grads"].double().abs().max())
+            per = sorted(((float((r0["grads"][o:o + n].double() / 2 - s["grads"][o:o + n].double()).abs().max()) / gmax,
+                           k) for k, (o, n) in s["offsets"].items()), reverse=True)[:4]
+            worst = " (worst: " + ", ".join(f"{k} {v:.1e}" for v, k in per) + ")"
+        check(e < tol, f"exchanged gradient rel {e:.2e} < {tol:g}{worst}")
     exact_path = phase == "step1" or (not bf16 and not any(flips.values()))
     if phase == "step1":
         # Adam normalises each element by sqrt(v): an element whose gradient nearly cancels across items keeps

@@ -49,8 +49,13 @@ def exchange(bucket: torch.Tensor, group=None) -> int:
     """Sum the bucket over ranks (no-op on one rank). Returns the world size (grad scale = 1/W)."""
     w = world_size(group)
     if w > 1:
-        # RCCL over xGMI ("nccl"); the gloo rehearsal / tests pass the same device bucket (torch's gloo stages
-        # it through pinned host memory on its own streams, ordered after the current stream like RCCL's)
+        # RCCL over xGMI ("nccl"): ordered on the current stream. The gloo rehearsal / tests pass the same
+        # device bucket; torch's gloo stages it through pinned host memory on a pool stream behind an event on
+        # the current stream — with the levels' streams joined into it, the 2-rank bf16 graph-warm-up test still
+        # read a gradient that differed by ~3e-4 in 2 of 3 runs, so the gloo path first finishes the producer
+        # stream on the host (no effect on the RCCL path)
+        if bucket.is_cuda and dist.get_backend(group) == dist.Backend.GLOO:
+            torch.cuda.current_stream(bucket.device).synchronize()
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return w
 
