@@ -330,27 +330,82 @@ struct RowStager {
   }
 };
 
-// Weights -> LDS image [K][O][C + pad] in T, with all global loads of a batch issued before any store.
+// Weights -> LDS image [K][O][C + pad] in T: 16-byte loads along the Keras kernel's contiguous axis, every
+// load of a batch issued before any store. DIRECT (w[k][c][o]: o contiguous) moves (tap, input-channel pair,
+// output quad) items — two float4 loads, four packed-pair stores; FLIP_T / PAIR (c contiguous) move (tap,
+// output channel, input quad) items — one float4 load, one 4-element store. (The per-element form — a scalar
+// load and a 2-byte store per weight — took ~5 us at the start of every workgroup: 0.41 ms of the step's
+// 1.98 ms of conv time, tools/conv_sweep.py.)
+template <class T> __device__ __forceinline__ void st2w(T* p, float a, float b);
+template <> __device__ __forceinline__ void st2w<float>(float* p, float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  *(f2*)p = f2{a, b};
+}
+template <> __device__ __forceinline__ void st2w<bf16>(bf16* p, float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  *(b2*)p = __builtin_convertvector((f2){a, b}, b2);
+}
+
 template <class T, int C, int O>
 __device__ __forceinline__ void stage_weights(const GatherArgs& a, T* wl, int WS) {
-  const int KOC = a.K * O * C;
-  for (int e0 = 0; e0 < KOC; e0 += 256 * 8) {
-    float wv[8];
+  static_assert(C % 4 == 0 && O % 4 == 0, "vector weight staging");
+  constexpr int NB = 4;  // items in flight per thread
+  if (a.wmode == W_DIRECT) {
+    constexpr int OQ = O / 4, CP = C / 2;
+    const int items = a.K * CP * OQ;
+    for (int e0 = 0; e0 < items; e0 += 256 * NB) {
+      f32x4 lo[NB], hi[NB];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = e0 + threadIdx.x + j * 256;
-      wv[j] = 0.f;
-      if (e < KOC) {
-        const int c = e % C, o = (e / C) % O, k = e / (C * O);
-        wv[j] = weff(a, k, c, o);
+      for (int j = 0; j < NB; ++j) {
+        const int e = e0 + threadIdx.x + j * 256;
+        lo[j] = hi[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e < items) {
+          const int oq = e % OQ, cp = (e / OQ) % CP, k = e / (OQ * CP);
+          const float* src = a.w + ((size_t)k * C + 2 * cp) * O + 4 * oq;
+          lo[j] = *(const f32x4*)src;
+          hi[j] = *(const f32x4*)(src + O);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int e = e0 + threadIdx.x + j * 256;
+        if (e < items) {
+          const int oq = e % OQ, cp = (e / OQ) % CP, k = e / (OQ * CP);
+          T* dst = wl + ((size_t)k * O + 4 * oq) * WS + 2 * cp;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st2w<T>(dst + i * WS, lo[j][i], hi[j][i]);
+        }
       }
     }
+  } else {
+    constexpr int CQ = C / 4;
+    const int items = a.K * O * CQ;
+    for (int e0 = 0; e0 < items; e0 += 256 * NB) {
+      f32x4 v[NB];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = e0 + threadIdx.x + j * 256;
-      if (e < KOC) {
-        const int c = e % C, o = (e / C) % O, k = e / (C * O);
-        wl[(k * O + o) * WS + c] = (T)wv[j];
+      for (int j = 0; j < NB; ++j) {
+        const int e = e0 + threadIdx.x + j * 256;
+        v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e < items) {
+          const int cq = e % CQ, o = (e / CQ) % O, k = e / (CQ * O);
+          const float* src = nullptr;
+          if (a.wmode == W_FLIP_T) {
+            src = a.w + ((size_t)(a.Kb - 1 - k) * O + o) * C + 4 * cq;
+          } else {  // PAIR: out pair column o = (p, ob) takes base tap kb = p + Pb - 2 (k - 1), zero outside
+            const int Ob = O >> 1, p = o >= Ob ? 1 : 0, ob = o - p * Ob, kb = p + a.Pb - 2 * (k - 1);
+            if (kb >= 0 && kb < a.Kb) src = a.w + ((size_t)kb * Ob + ob) * C + 4 * cq;
+          }
+          if (src) v[j] = *(const f32x4*)src;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int e = e0 + threadIdx.x + j * 256;
+        if (e < items) {
+          const int cq = e % CQ, o = (e / CQ) % O, k = e / (CQ * O);
+          st4<T>(wl + ((size_t)k * O + o) * WS + 4 * cq, v[j]);
+        }
       }
     }
   }
@@ -1418,6 +1473,7 @@ static int launch_conv32_n(const GatherArgs& a, int nep, hipStream_t s, int* nwg
 
 // x chunks per thread the 32-channel kernel stages for this launch (0: not applicable)
 static int conv32_pvx(const GatherArgs& a, int dtype, bool fw) {
+  if ((uintptr_t)a.w & 15) return 0;  // stage_weights reads the kernel in 16-byte vectors
   const bool o64 = a.O == 64 && !fw && (a.wmode != W_PAIR || a.T_full <= 2 * a.T_out);
   if (a.C != 32 || !((a.O == 32 && a.wmode != W_PAIR) || o64) || a.K > 4 || a.S > 2) return 0;
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return 0;
@@ -1454,6 +1510,7 @@ static int launch_conv32(const GatherArgs& a, int pvx, hipStream_t s, int* nwg_o
 }
 
 static bool mfma_ok(const GatherArgs& a, int dtype) {
+  if ((uintptr_t)a.w & 15) return false;  // stage_weights reads the kernel in 16-byte vectors
   if (a.flags & (VQA_X_F32 | VQA_Y_F32)) return false;
   if (a.K > 4) return false;  // the kernel's tap loop is unrolled for K <= 4
   if (!((a.C == 32 || a.C == 64) && (a.O == 32 || a.O == 64 || a.O == 128))) return false;
