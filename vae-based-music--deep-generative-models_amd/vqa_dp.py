@@ -49,13 +49,17 @@ def exchange(bucket: torch.Tensor, group=None) -> int:
     """Sum the bucket over ranks (no-op on one rank). Returns the world size (grad scale = 1/W)."""
     w = world_size(group)
     if w > 1:
-        # RCCL over xGMI ("nccl"): ordered on the current stream. The gloo rehearsal / tests pass the same
-        # device bucket; torch's gloo stages it through pinned host memory on a pool stream behind an event on
-        # the current stream — with the levels' streams joined into it, the 2-rank bf16 graph-warm-up test still
-        # read a gradient that differed by ~3e-4 in 2 of 3 runs, so the gloo path first finishes the producer
-        # stream on the host (no effect on the RCCL path)
+        # RCCL over xGMI ("nccl"): ordered on the current stream, on the device bucket. The gloo rehearsal
+        # backend (tests, bench under VQA_DIST_BACKEND=gloo) stages the bucket through host memory itself: a
+        # blocking copy out on the producer stream (which has joined the levels' streams), the CPU all_reduce,
+        # and a copy back on the same stream. Handing gloo the device bucket (its own pinned staging on a pool
+        # stream behind an event) left the 2-rank bf16 graph-warm-up test with a sum that missed part of the
+        # last-produced gradients (level 2, encoder block 0) in a few runs, even after a host sync first.
         if bucket.is_cuda and dist.get_backend(group) == dist.Backend.GLOO:
-            torch.cuda.current_stream(bucket.device).synchronize()
+            host = bucket.to("cpu")  # synchronous: waits for the producer stream
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            bucket.copy_(host)
+            return w
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return w
 
