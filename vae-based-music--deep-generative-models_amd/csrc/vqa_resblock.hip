@@ -766,7 +766,10 @@ static int rs_cus() {
   return n;
 }
 constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the partial rows)
-constexpr int kResMinTiles = 4;  // backward: tiles per workgroup at least (bounds the partial rows of short launches)
+// backward: tiles per workgroup at least (bounds the partial rows of short launches). 2 against 4, 3 and 1 in
+// alternating same-box runs: 7.316 ms/step (5 runs) vs 7.363 (4), 7.355 (3), 7.369 (1): level 2's short launches
+// (T <= 4096) are latency-bound chains of tiles per workgroup
+constexpr int kResMinTiles = 2;
 
 // + one trash row for the staging chunks past a tile's rows (Rows32Buf)
 static size_t fwd_lds(int d, int esz, int rt) {
