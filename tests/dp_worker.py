@@ -89,7 +89,23 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = build(B_LOCAL, config=config, dtype=dtype)
     xs = [x[rank * B_LOCAL:(rank + 1) * B_LOCAL] for x in batches(world, config)]
+    local = []
+    if os.environ.get("VQA_DP_PROBE") == "1":
+        # the RCCL branch's contract: at the exchange, the bucket as seen IN ORDER on the current stream (no
+        # host sync) holds this rank's complete local gradient — a device copy queued there records it
+        import vqa_dp
+        P = m.layout["grads"][1]
+        exchange = vqa_dp.exchange
+
+        def probe(bucket, group=None):
+            if bucket.numel() > P:
+                local.append(bucket[:P].detach().clone())
+            return exchange(bucket, group)
+
+        vqa_dp.exchange = probe
     res = run(m, xs, mode)
+    if local:
+        res["local_step1"] = local[0].cpu()
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

@@ -50,13 +50,13 @@ def _port():
     return p
 
 
-def _run_ranks(mode, tmp_path, config, dtype, world=2):
+def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False):
     port = _port()
     procs, outs = [], []
     for r in range(world):
         out = str(tmp_path / f"{mode}_{config}_{dtype}_rank{r}.pt")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), VQA_DP_PROBE="1" if probe else "0")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out, config, dtype],
                                       env=env))
         outs.append(out)
@@ -206,6 +206,31 @@ def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode, config, d
         print("\n".join(rep))
         failures += [f"{phase}: {b}" for b in bad]
     assert not failures, failures
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_exchange_sees_complete_local_gradient_on_stream(cuda, tmp_path, mode):
+    """The stream-ordering contract the RCCL branch (`vqa_dp.exchange`: all_reduce on the device bucket, ordered
+    on the current stream) relies on: at the exchange of the benched architecture's bf16 step (3 levels on their
+    own streams, joined into the producer stream; eager, and the graph-capture warm-up on a side stream), a
+    device copy of the bucket queued on the current stream WITHOUT a host sync equals, bitwise, one process
+    computing that rank's half of the batch (same shapes, deterministic kernels). The gloo rehearsal stages the
+    bucket through host memory after this point, so the copy is what an RCCL all_reduce would read."""
+    config, dtype = "cfg2_short", "bf16"
+    ranks = _run_ranks(mode, tmp_path, config, dtype, probe=True)
+    xs = W.batches(2, config)[0]
+    for r in range(2):
+        m = W.build(W.B_LOCAL, config=config, dtype=dtype)
+        m._compute(m._as_input(xs[r * W.B_LOCAL:(r + 1) * W.B_LOCAL]), True)
+        torch.cuda.synchronize()
+        want = m.bucket[:m.layout["grads"][1]].detach().cpu()
+        del m
+        got = ranks[r]["local_step1"]
+        n = int((got != want).sum())
+        assert n == 0, f"rank {r}: {n} of {want.numel()} gradient elements differ at the exchange " \
+                       f"(max {float((got - want).abs().max()):.3e})"
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.timeout(600)
