@@ -322,6 +322,7 @@ extern "C" int vqa_layernorm_fwd(const void* x, const float* gamma, const float*
 }
 
 extern "C" size_t vqa_layernorm_bwd_workspace(int64_t rows, int C) {
+  if (rows < 1 || C < 1) return 0;
   return (size_t)ln_wgs(rows) * 2 * (size_t)C * sizeof(float);
 }
 

@@ -1820,6 +1820,7 @@ int run_wgrad(const void* x, const void* g, float* dw, float* db, int B, int T_i
 }
 
 size_t wgrad_ws(int dtype, int B, int T_in, int T_out, int C, int O, int K, int S, int D, int flags) {
+  if (B < 1 || T_in < 1 || T_out < 1 || C < 1 || O < 1 || K < 1 || S < 1 || D < 1) return 0;  // no such conv
   return plan_wgrad(dtype, B, T_in, T_out, C, O, K, S, D, flags).ws_bytes;
 }
 
@@ -1829,8 +1830,13 @@ size_t wgrad_ws(int dtype, int B, int T_in, int T_out, int C, int O, int K, int 
 // C ABI
 using namespace vqa;
 
-extern "C" int vqa_same_out_len(int T_in, int stride) { return (T_in + stride - 1) / stride; }
+// -1 for a shape TF's "same" padding does not define (stride or dilation < 1, K < 1, T_in < 0)
+extern "C" int vqa_same_out_len(int T_in, int stride) {
+  if (stride < 1 || T_in < 0) return -1;
+  return (T_in + stride - 1) / stride;
+}
 extern "C" int vqa_same_pad_left(int T_in, int K, int stride, int dilation) {
+  if (stride < 1 || dilation < 1 || K < 1 || T_in < 0) return -1;
   const int out = (T_in + stride - 1) / stride;
   const int pad = std::max((out - 1) * stride + (K - 1) * dilation + 1 - T_in, 0);
   return pad / 2;
@@ -1839,6 +1845,8 @@ extern "C" int vqa_same_pad_left(int T_in, int K, int stride, int dilation) {
 extern "C" int vqa_conv1d_fwd(const void* x, const float* w, const float* bias, const void* residual, void* y, int B,
                               int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation, int pad_left,
                               int flags, int dtype, vqa_stream_t stream) {
+  VQA_ARG(stride >= 1 && dilation >= 1 && K >= 1, "conv1d_fwd: stride %d, dilation %d, K %d must be >= 1", stride,
+          dilation, K);
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_fwd: T_out %d != ceil(T_in/stride)", T_out);
   if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags) && (dtype == VQA_F32 || dtype == VQA_BF16)) {
     VQA_ARG(x && w && y && B > 0 && T_in > 0, "conv1d_fwd: bad arguments");
@@ -1862,6 +1870,8 @@ static int swap_xy_flags(int flags) {
 extern "C" int vqa_conv1d_bwd_data(const void* dy, const float* w, const void* mask, const void* residual, void* dx,
                                    int B, int T_in, int T_out, int C_in, int C_out, int K, int stride, int dilation,
                                    int pad_left, int flags, int dtype, vqa_stream_t stream) {
+  VQA_ARG(stride >= 1 && dilation >= 1 && K >= 1, "conv1d_bwd_data: stride %d, dilation %d, K %d must be >= 1", stride,
+          dilation, K);
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_data: T_out %d != ceil(T_in/stride)", T_out);
   if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags) && (dtype == VQA_F32 || dtype == VQA_BF16)) {
     VQA_ARG(dy && w && dx && B > 0 && T_in > 0, "conv1d_bwd_data: bad arguments");
@@ -1895,6 +1905,8 @@ extern "C" size_t vqa_conv1d_bwd_weight_workspace(int B, int T_in, int T_out, in
 extern "C" int vqa_conv1d_bwd_weight(const void* x, const void* dy, float* dw, float* db, int B, int T_in, int T_out,
                                      int C_in, int C_out, int K, int stride, int dilation, int pad_left, int flags,
                                      int dtype, void* workspace, size_t ws_bytes, vqa_stream_t stream) {
+  VQA_ARG(stride >= 1 && dilation >= 1 && K >= 1, "conv1d_bwd_weight: stride %d, dilation %d, K %d must be >= 1", stride,
+          dilation, K);
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_weight: T_out %d != ceil(T_in/stride)", T_out);
   return run_wgrad(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
                    flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, (hipStream_t)stream,
@@ -1949,6 +1961,8 @@ extern "C" int vqa_conv1d_bwd_weight_partials(const void* x, const void* dy, flo
                                               int pad_left, int flags, int dtype, void* workspace, size_t ws_bytes,
                                               vqa_partials_desc* desc, vqa_stream_t stream) {
   VQA_ARG(desc, "bwd_weight_partials: NULL descriptor");
+  VQA_ARG(stride >= 1 && dilation >= 1 && K >= 1, "conv1d_bwd_weight: stride %d, dilation %d, K %d must be >= 1", stride,
+          dilation, K);
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_weight: T_out %d != ceil(T_in/stride)", T_out);
   return run_wgrad(x, dy, dw, db, B, T_in, T_out, C_in, C_out, K, stride, dilation, pad_left,
                    flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32), dtype, workspace, ws_bytes, (hipStream_t)stream,
@@ -1987,6 +2001,7 @@ static GatherArgs fused_bwd_args(const void* dy, const float* w, const void* x, 
 
 extern "C" size_t vqa_conv1d_bwd_data_weight_workspace(int B, int T_in, int T_out, int C_in, int C_out, int K,
                                                        int stride, int dilation, int pad_left, int flags, int dtype) {
+  if (B < 1 || T_in < 1 || T_out < 1 || C_in < 1 || C_out < 1 || K < 1 || stride < 1 || dilation < 1) return 0;
   size_t need = wgrad_ws(dtype, B, T_in, T_out, C_in, C_out, K, stride, dilation,
                          flags & (VQA_PRE_RELU | VQA_X_F32 | VQA_Y_F32));
   if (co1_supported(C_in, C_out, K, stride, dilation, dtype, flags)) need = std::max(need, co1_bwd_workspace(C_in, K));
@@ -2003,6 +2018,8 @@ extern "C" int vqa_conv1d_bwd_data_weight(const void* dy, const float* w, const 
                                           int C_out, int K, int stride, int dilation, int pad_left, int flags,
                                           int dtype, void* workspace, size_t ws_bytes, vqa_partials_desc* desc,
                                           vqa_stream_t stream) {
+  VQA_ARG(stride >= 1 && dilation >= 1 && K >= 1, "conv1d_bwd_data_weight: stride %d, dilation %d, K %d must be >= 1", stride,
+          dilation, K);
   VQA_ARG(T_out == (T_in + stride - 1) / stride, "conv1d_bwd_data_weight: T_out %d != ceil(T_in/stride)", T_out);
   VQA_ARG(dy && w && x && dx && dw, "conv1d_bwd_data_weight: null tensor pointer");
   VQA_ARG(dtype == VQA_F32 || dtype == VQA_BF16, "unknown dtype %d", dtype);

@@ -403,6 +403,7 @@ extern "C" int vqa_dtail_supported(int C, int Cu, int K_up, int stride_up, int K
 }
 
 extern "C" size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype) {
+  if (B < 1 || T < 1) return 0;
   (void)C;
   (void)Cu;
   (void)dtype;

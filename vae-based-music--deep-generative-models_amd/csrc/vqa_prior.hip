@@ -1946,6 +1946,7 @@ extern "C" int vqa_seqlin_fwd_ln_prepped(const void* x, int64_t ldx, const float
 }
 
 extern "C" size_t vqa_seqlin_wgrad_workspace(int nseq, int T, int K, int N, int taps) {
+  if (nseq < 1 || T < 1 || K < 1 || N < 1 || taps < 1) return 0;
   int seg_rows, segs;
   wgrad_plan(nseq, T, seg_rows, segs);
   return (size_t)nseq * segs * ((size_t)taps * K * N + N) * sizeof(float);
@@ -2161,6 +2162,7 @@ static int head_segs(int64_t M, int V) {
 }
 
 extern "C" size_t vqa_head_bwd_workspace(int64_t M, int K, int V) {
+  if (M < 1 || K < 1 || V < 1) return 0;
   return (size_t)head_segs(M, V) * ((size_t)K * V + V) * sizeof(float);
 }
 
@@ -2193,6 +2195,7 @@ extern "C" int vqa_head_bwd(const void* x, const void* wt, const float* bias, co
 }
 
 extern "C" size_t vqa_rowsum_workspace(int64_t rows, int64_t n) {
+  if (rows < 1 || n < 1) return 0;
   return (size_t)rows * ((n + kRowsumChunk - 1) / kRowsumChunk) * sizeof(float);
 }
 
@@ -2213,6 +2216,7 @@ extern "C" int vqa_rowsum(const float* x, int64_t rows, int64_t n, float scale, 
 constexpr size_t kDecComposed = (size_t)3 * kDecW * 3 * kDecAW + 3 * kDecAW + kDecAW * kDecW + kDecW;  // floats/layer
 
 extern "C" size_t vqa_prior_decode_cache_bytes(int N, int depth, int ctx) {
+  if (N < 1 || depth < 1 || ctx < 1) return 0;
   return ((size_t)2 * N * depth * ctx * kDecAW + (size_t)depth * kDecComposed) * sizeof(float);
 }
 

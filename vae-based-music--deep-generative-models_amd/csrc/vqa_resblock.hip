@@ -866,6 +866,7 @@ extern "C" int vqa_resblock_fwd(const void* x, const float* wa, const float* ba,
 }
 
 extern "C" size_t vqa_resblock_bwd_workspace(int B, int T, int C, int dilation, int dtype) {
+  if (C < 1) return 0;
   (void)B;
   (void)T;
   (void)dilation;

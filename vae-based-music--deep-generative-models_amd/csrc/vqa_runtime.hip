@@ -161,7 +161,7 @@ using namespace vqa;
 extern "C" const char* vqa_get_last_error(void) { return g_err; }
 extern "C" const char* vqa_version(void) { return "libvqa 0.1 gfx950"; }
 
-extern "C" size_t vqa_mse_loss_workspace(int64_t n) { return (size_t)blocks_for(n, 1024) * sizeof(float); }
+extern "C" size_t vqa_mse_loss_workspace(int64_t n) { return n < 1 ? 0 : (size_t)blocks_for(n, 1024) * sizeof(float); }
 
 extern "C" int vqa_mse_loss(const float* x, const float* r, const float* extra_grad, float* dr, float* loss_out,
                             int64_t n, void* workspace, size_t ws_bytes, vqa_stream_t stream) {

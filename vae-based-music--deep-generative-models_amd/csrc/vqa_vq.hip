@@ -775,6 +775,7 @@ extern "C" int vqa_vq_argmin_split(const void* z, const void* E3, const float* e
 }
 
 extern "C" size_t vqa_vq_quantize_workspace(int64_t N, int D, int K, int dtype) {
+  if (N < 1 || D < 1 || K < 1) return 0;
   (void)dtype;
   return align256((size_t)quantize_blocks((long long)N * D) * sizeof(float)) + sort_ws_bytes(N, D, K);
 }
@@ -871,7 +872,9 @@ extern "C" int64_t vqa_reset_perm_index(uint64_t seed, int64_t counter, int leve
   return perm_index(perm_key(seed, counter, level), M, k);
 }
 
-extern "C" size_t vqa_embedding_bwd_workspace(int64_t N, int D, int K) { return sort_ws_bytes(N, D, K); }
+extern "C" size_t vqa_embedding_bwd_workspace(int64_t N, int D, int K) {
+  return N < 1 || D < 1 || K < 1 ? 0 : sort_ws_bytes(N, D, K);
+}
 
 extern "C" int vqa_embedding_bwd(const void* dy, const int64_t* idx, float* dtable, int64_t N, int D, int K, int dtype,
                                  void* workspace, size_t ws_bytes, vqa_stream_t stream) {
