@@ -54,6 +54,11 @@ def parse():
     p.add_argument("--cpu-batch", type=int, default=8)
     p.add_argument("--cpu-steps", type=int, default=4)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--no-prior", action="store_true", help="skip the config-4 / config-5 legs")
+    p.add_argument("--prior-batch", type=int, default=8, help="config-4 leg: sequences per GPU")
+    p.add_argument("--prior-steps", type=int, default=10)
+    p.add_argument("--decode-samples", type=int, default=16)
+    p.add_argument("--decode-len", type=int, default=1024)
     return p.parse_args()
 
 
@@ -155,6 +160,77 @@ def cpu_baseline(batch, steps, seq):
                       f"affinity mask, OMP_NUM_THREADS {omp or 'unset'}; {dt:.1f} s)"}
 
 
+def prior_legs(a, dev, world, rank):
+    """BASELINE configs 4 and 5 beside the config-2 line (extra keys; `value` stays config 2's):
+      config4_prior_train: SMALL_PRIOR (width 128, depth 6, 2 heads, 4 blocks, 2048 bins) Prior.train_step over
+        ctx = 8192 top-level codes, `prior_batch` sequences per GPU, bf16, the whole step (both teacher-forcing
+        passes, backward, Keras Adam) replayed from a hipGraph; under DP two graphs around the one all_reduce of
+        the prior's bucket (weak scaling, the same barrier + max-over-ranks clock as the main line);
+      config5_upsampler_decode (rank 0, N = 1): the SMALL_UPSAMPLER form (the same transformer conditioned on the
+        level above through ConditionerNet) drawing `decode_samples` samples x `decode_len` positions by ancestral
+        sampling, one persistent decode launch per window (prior.py:374-408, Sampler.py:72-109).
+    Synthetic uniform codes, random-init weights (prior.py:240-335)."""
+    from prior import FMHABasedAutoregressiveModel, Prior
+    kw = dict(width=128, depth=6, heads=2, blocks=4, attn_stacks=1, drop_out_rate=0.0)
+    ctx, bins = 8192, 2048
+    out = {}
+    pr = Prior(2, [(ctx * 16,), (ctx * 4,), (ctx,)], bins, [3, 2, 2], [2, 2, 2], None, kw, None, dtype=a.dtype,
+               device=dev)  # under DP the default process group (vqa_dp)
+    g = torch.Generator(device=dev).manual_seed(11 + rank)
+    codes = torch.randint(0, bins - 1, (a.prior_batch, ctx), device=dev, generator=g)
+    pr.capture_train_step(codes, warmup=1)
+    pr.train_step(codes)  # the first replay uploads the graph
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.prior_steps):
+        pr.train_step(codes)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    tok = a.prior_batch * ctx * a.prior_steps * world / el
+    out["config4_prior_train"] = {
+        "metric": "tokens/s prior train step (SMALL_PRIOR, ctx 8192), whole job", "value": round(tok, 1),
+        "value_per_gpu": round(tok / world, 1), "unit": "tokens/s", "n_gpus": world, "steps": a.prior_steps,
+        "ms_per_step": round(el / a.prior_steps * 1e3, 3), "dtype": a.dtype, "scaling": "weak",
+        "config": {"workload": "BASELINE config 4", "batch_per_gpu": a.prior_batch, "ctx": ctx, "bins": bins,
+                   "parallelism": f"dp{world}", "graph": True, **kw},
+        "loss": round(float(pr.results()["loss"]), 5)}
+    del pr
+    torch.cuda.empty_cache()
+    if world == 1 and rank == 0:
+        m = FMHABasedAutoregressiveModel(bins, 128, 6, 4, heads=2, attn_stacks=1, drop_out_rate=0.0,
+                                         context_length=(ctx,), level=0, levels=2, zq_shapes=[(ctx,), (ctx // 4,)],
+                                         downs=[3, 2], strides=[2, 2],
+                                         cond_kwargs=dict(dilation_factor=3, dilation_cycle=4, residual_width=32,
+                                                          residual_depth=8), dtype="fp32", device=dev)
+        g = torch.Generator(device=dev).manual_seed(2)
+        up = torch.randint(0, bins - 1, (a.decode_samples, ctx // 4), device=dev, generator=g)
+        m.sample(a.decode_samples, max_length=16, x_cond=up, seed=1)  # warm-up: conditioner + decode kernels
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        toks = m.sample(a.decode_samples, max_length=a.decode_len, x_cond=up, seed=2)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out["config5_upsampler_decode"] = {
+            "metric": "tokens/s ancestral decode (upsampler prior + ConditionerNet)",
+            "value": round(a.decode_samples * a.decode_len / el, 1), "unit": "tokens/s", "n_gpus": 1,
+            "ms_per_position": round(el / a.decode_len * 1e3, 4), "samples": a.decode_samples,
+            "positions": a.decode_len, "dtype": "fp32 (decode)",
+            "config": {"workload": "BASELINE config 5 (one window, conditioner included)", "ctx": ctx, "bins": bins,
+                       **kw},
+            "tokens_in_range": bool(((toks >= 0) & (toks < bins)).all())}
+        del m
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -250,6 +326,13 @@ def main():
                         "frac": round(fl / (us_total * 1e-6) / 1e12 / BF16_DENSE_TFLOPS, 4),
                         "busy_frac_pmc": pmc.get("mfma_busy_frac")}
 
+    legs = {}
+    if not a.no_prior:
+        try:
+            legs = prior_legs(a, dev, world, rank)
+        except Exception as e:  # an extra leg must never cost the config-2 line
+            legs = {"prior_legs_error": f"{type(e).__name__}: {e}"[:400]}
+
     out = None
     if rank == 0:
         cpu = None
@@ -270,7 +353,7 @@ def main():
                           "model": "VQVAE levels=3 latent=64 K=2048 down_depth=[3,2,2] width=32 depth=4 dil=3",
                           "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",
                           "graph": not a.no_graph, "final_loss": round(loss, 5)},
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "cpu_baseline": cpu, **legs}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -48,6 +48,11 @@ enum {
 /* ---- library -------------------------------------------------------------------------------- */
 const char* vqa_get_last_error(void);
 const char* vqa_version(void);
+/* ABI revision of the signatures in this header. It is raised whenever an existing entry point's argument
+ * list changes (revision 2: vqa_adam_keras gained lr_dev, vqa_dropout / vqa_prior_embed_fwd elem_offset,
+ * vqa_prior_decode out_ld); a binding built against another revision must refuse the library. */
+#define VQA_ABI_VERSION 2
+int vqa_abi_version(void);
 /* TF SAME padding (Appendix A.2 of SURVEY.md): left pad of a conv with these parameters. Host-only. */
 int vqa_same_pad_left(int T_in, int K, int stride, int dilation);
 int vqa_same_out_len(int T_in, int stride);

@@ -21,9 +21,14 @@ CONFIGS = {
                  residual_width=32, residual_depth=4, dilation_factor=3),
     "cfg2_short": dict(input_len=8192, levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2],
                        num_embeddings=2048, residual_width=32, residual_depth=4, dilation_factor=3),
+    # BASELINE config 3's per-rank workload: config 2 at its full chunk length (run with VQA_DP_BATCH=32)
+    "cfg2": dict(input_len=65536, levels=3, latent_dim=64, down_depth=[3, 2, 2], strides=[2, 2, 2],
+                 num_embeddings=2048, residual_width=32, residual_depth=4, dilation_factor=3),
 }
 CFG = CONFIGS["cfg1"]
-B_LOCAL = 2
+B_LOCAL = int(os.environ.get("VQA_DP_BATCH", "2"))  # items per rank
+# "all": step 1, step 2, forward-only EMA call; "step1": the first step only (full-size runs)
+PHASES = os.environ.get("VQA_DP_PHASES", "all")
 
 
 def build(B, process_group=None, config="cfg1", dtype="fp32"):
@@ -66,11 +71,15 @@ def run(m, xs, mode):
         m.train_step(xs[0])
         torch.cuda.synchronize()
         res["step1"] = snapshot(m)
+        if PHASES == "step1":
+            return res
         m.train_step(xs[1])
     else:
         m.capture_train_step(xs[0], warmup=1)
         torch.cuda.synchronize()
         res["step1"] = snapshot(m)
+        if PHASES == "step1":
+            return res
         m.train_step(xs[1])
     torch.cuda.synchronize()
     res["steps"] = snapshot(m)
@@ -89,23 +98,29 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = build(B_LOCAL, config=config, dtype=dtype)
     xs = [x[rank * B_LOCAL:(rank + 1) * B_LOCAL] for x in batches(world, config)]
-    local = []
+    local, post = [], []
     if os.environ.get("VQA_DP_PROBE") == "1":
-        # the RCCL branch's contract: at the exchange, the bucket as seen IN ORDER on the current stream (no
-        # host sync) holds this rank's complete local gradient — a device copy queued there records it
+        # the exchange's stream contract, both sides, as device copies queued IN ORDER on the current stream
+        # (no host sync): at entry the bucket holds this rank's complete local gradient (what RCCL reads), and
+        # right after `exchange` returns it holds the sum over ranks (what `_update` / the second graph reads)
         import vqa_dp
         P = m.layout["grads"][1]
         exchange = vqa_dp.exchange
 
         def probe(bucket, group=None):
-            if bucket.numel() > P:
+            full = bucket.numel() > P
+            if full:
                 local.append(bucket[:P].detach().clone())
-            return exchange(bucket, group)
+            w = exchange(bucket, group)
+            if full:
+                post.append(bucket[:P].detach().clone())
+            return w
 
         vqa_dp.exchange = probe
     res = run(m, xs, mode)
     if local:
         res["local_step1"] = local[0].cpu()
+        res["post_step1"] = post[0].cpu()
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

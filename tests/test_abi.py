@@ -32,6 +32,15 @@ def test_version_and_error_string():
     assert isinstance(V.last_error(), str)
 
 
+def test_abi_revision_matches_header_and_binding():
+    """include/vqa.h VQA_ABI_VERSION = the library's vqa_abi_version() = the binding's ABI_VERSION; a library of
+    another revision is refused at load (a changed argument list would otherwise shift arguments silently)."""
+    import re
+    hdr = open(HEADER).read()
+    want = int(re.search(r"#define VQA_ABI_VERSION (\d+)", hdr).group(1))
+    assert V.lib().vqa_abi_version() == want == V.ABI_VERSION
+
+
 @pytest.mark.parametrize("T,K,s,d", [(4096, 4, 2, 1), (4097, 4, 2, 1), (512, 3, 1, 27), (40, 3, 1, 27),
                                      (1000, 3, 1, 9), (7, 4, 2, 1), (65536, 3, 1, 1), (1, 3, 1, 1)])
 def test_same_padding_matches_oracle(T, K, s, d):

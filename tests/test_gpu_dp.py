@@ -50,13 +50,14 @@ def _port():
     return p
 
 
-def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False):
+def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False, batch=2, phases="all"):
     port = _port()
     procs, outs = [], []
     for r in range(world):
         out = str(tmp_path / f"{mode}_{config}_{dtype}_rank{r}.pt")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), VQA_DP_PROBE="1" if probe else "0")
+                   MASTER_PORT=str(port), VQA_DP_PROBE="1" if probe else "0", VQA_DP_BATCH=str(batch),
+                   VQA_DP_PHASES=phases)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out, config, dtype],
                                       env=env))
         outs.append(out)
@@ -69,7 +70,7 @@ _SINGLE = {}
 
 
 def _single(config, dtype, world=2):
-    key = (config, dtype)
+    key = (config, dtype, world)
     if key not in _SINGLE:
         m = W.build(W.B_LOCAL * world, config=config, dtype=dtype)
         _SINGLE[key] = W.run(m, W.batches(world, config), "eager")
@@ -91,8 +92,10 @@ def _l2(a, b):
 CASES = [("cfg1", "fp32"), ("cfg2_short", "fp32"), ("cfg2_short", "bf16")]
 
 
-def _compare(r0, r1, s, K, D, L, phase, bf16):
-    """-> (report lines, failures) of one phase's rank-0 / rank-1 / single-process snapshots."""
+def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False):
+    """-> (report lines, failures) of one phase's rank-0 / rank-1 / single-process snapshots. `strict` (BASELINE
+    config 1's architecture in fp32, which has no near-tie rows on these batches): after every phase the code
+    counts stay bitwise equal and the weights within rel 1e-5 of max |w|, as in the first DP tests."""
     lr = 1e-3  # Keras Adam default (vqa_optim.Adam)
     nst = 2 * K * D + K  # one level's stats region: m_sumT, n_sum, RT
     rep, bad = [], []
@@ -127,7 +130,10 @@ def _compare(r0, r1, s, K, D, L, phase, bf16):
             # step 2 runs on weights that differ in their last bits (summation grouping of step 1's gradient):
             # a row whose two nearest codes are within that rounding may take the other one
             lim = 2e-2 if bf16 else 5e-3
-            check(moved <= lim * rows, f"level {l}: {moved:.0f} of {rows:.0f} rows changed code (<= {lim:g})")
+            if strict:
+                check(moved == 0, f"level {l}: code counts bitwise ({rows:.0f} rows)")
+            else:
+                check(moved <= lim * rows, f"level {l}: {moved:.0f} of {rows:.0f} rows changed code (<= {lim:g})")
             e = _rel(RT, ss[K * D + K:])
             check(e < (2e-2 if bf16 else 2e-3), f"level {l}: reset rows rel {e:.2e}")
             # the EMA sums of every code whose count is unchanged (the moved rows are accounted for above)
@@ -147,6 +153,8 @@ def _compare(r0, r1, s, K, D, L, phase, bf16):
             worst = " (worst: " + ", ".join(f"{k} {v:.1e}" for v, k in per) + ")"
         check(e < tol, f"exchanged gradient rel {e:.2e} < {tol:g}{worst}")
     exact_path = phase == "step1" or (not bf16 and not any(flips.values()))
+    if strict:
+        check(exact_path, "exact path (no code moved)")
     if phase == "step1":
         # Adam normalises each element by sqrt(v): an element whose gradient nearly cancels across items keeps
         # its absolute rounding noise but has a small sqrt(v), so a 1e-7-relative gradient difference becomes
@@ -164,6 +172,9 @@ def _compare(r0, r1, s, K, D, L, phase, bf16):
         check(dw <= 2 * lr * 1.01, f"max |delta w| {dw:.2e} <= two Adam updates ({2 * lr:g})")
         e = _l2(r0["weights"], s["weights"])
         check(e < 1e-5, f"weights relative L2 {e:.2e} < 1e-5")
+        if strict:
+            e = _rel(r0["weights"], s["weights"])
+            check(e < 1e-5, f"weights rel {e:.2e} < 1e-5 (max-norm)")
         if phase != "forward":
             e = max(_l2(r0["adam_m"], s["adam_m"]), _l2(r0["adam_v"], s["adam_v"]))
             check(e < 1e-5, f"Adam moments relative L2 {e:.2e} < 1e-5")
@@ -201,7 +212,8 @@ def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode, config, d
     ref = _single(config, dtype)
     failures = []
     for phase in ("step1", "steps", "forward"):
-        rep, bad = _compare(ranks[0][phase], ranks[1][phase], ref[phase], K, D, L, phase, dtype == "bf16")
+        rep, bad = _compare(ranks[0][phase], ranks[1][phase], ref[phase], K, D, L, phase, dtype == "bf16",
+                            strict=(config, dtype) == ("cfg1", "fp32"))
         print(f"--- {config} {dtype} {mode} {phase}")
         print("\n".join(rep))
         failures += [f"{phase}: {b}" for b in bad]
@@ -210,27 +222,86 @@ def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode, config, d
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("mode", ["eager", "graph"])
-def test_exchange_sees_complete_local_gradient_on_stream(cuda, tmp_path, mode):
-    """The stream-ordering contract the RCCL branch (`vqa_dp.exchange`: all_reduce on the device bucket, ordered
-    on the current stream) relies on: at the exchange of the benched architecture's bf16 step (3 levels on their
-    own streams, joined into the producer stream; eager, and the graph-capture warm-up on a side stream), a
-    device copy of the bucket queued on the current stream WITHOUT a host sync equals, bitwise, one process
-    computing that rank's half of the batch (same shapes, deterministic kernels). The gloo rehearsal stages the
-    bucket through host memory after this point, so the copy is what an RCCL all_reduce would read."""
+def test_exchange_stream_contract_both_sides(cuda, tmp_path, mode):
+    """The stream-ordering contract of `vqa_dp.exchange` on both sides, at the benched architecture's bf16 step
+    (3 levels on their own streams, joined into the producer stream; eager, and the graph-capture warm-up on a
+    side stream), as device copies of the bucket queued on the current stream WITHOUT a host sync:
+      producer side — at entry the copy equals, bitwise, one process computing that rank's half of the batch
+        (same shapes, deterministic kernels): what an RCCL all_reduce reads;
+      consumer side — right after `exchange` returns the copy equals, bitwise, the sum of the two ranks'
+        single-process local gradients (fp32 a + b is commutative, so any 2-rank reduction gives it): what Keras
+        Adam (`_update`, eager) and the second graph (`g2.replay()`) read next on that stream."""
     config, dtype = "cfg2_short", "bf16"
     ranks = _run_ranks(mode, tmp_path, config, dtype, probe=True)
     xs = W.batches(2, config)[0]
+    wants = []
     for r in range(2):
         m = W.build(W.B_LOCAL, config=config, dtype=dtype)
         m._compute(m._as_input(xs[r * W.B_LOCAL:(r + 1) * W.B_LOCAL]), True)
         torch.cuda.synchronize()
-        want = m.bucket[:m.layout["grads"][1]].detach().cpu()
+        wants.append(m.bucket[:m.layout["grads"][1]].detach().cpu())
         del m
+    for r in range(2):
         got = ranks[r]["local_step1"]
-        n = int((got != want).sum())
-        assert n == 0, f"rank {r}: {n} of {want.numel()} gradient elements differ at the exchange " \
-                       f"(max {float((got - want).abs().max()):.3e})"
+        n = int((got != wants[r]).sum())
+        assert n == 0, f"rank {r}: {n} of {got.numel()} gradient elements differ at the exchange " \
+                       f"(max {float((got - wants[r]).abs().max()):.3e})"
+    total = wants[0] + wants[1]
+    for r in range(2):
+        got = ranks[r]["post_step1"]
+        n = int((got != total).sum())
+        assert n == 0, f"rank {r}: {n} of {got.numel()} elements of the exchanged bucket, read on the current " \
+                       f"stream after the exchange, differ from local0 + local1 (max {float((got - total).abs().max()):.3e})"
     torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(600)
+def test_dp4_reset_rows_from_every_rank_offset(cuda, tmp_path):
+    """Four ranks (gloo, all on cuda:0) on the benched architecture's short-chunk form in fp32: the global reset
+    rows come from rank offsets 0-3 (vqa_dp.global_row_range; level 2 has N_global = 512 < K = 2048, the _tile
+    path over the global batch, VectorQuantizer.py:137,191-199), and every phase ends where one process on the
+    concatenated batch of 8 ends, with the bounds of test_dp2_matches_single_process_global_batch."""
+    config, dtype = "cfg2_short", "fp32"
+    cfg = W.CONFIGS[config]
+    K, D, L = cfg["num_embeddings"], cfg["latent_dim"], cfg["levels"]
+    ranks = _run_ranks("graph", tmp_path, config, dtype, world=4)
+    ref = _single(config, dtype, world=4)
+    failures = []
+    for phase in ("step1", "steps", "forward"):
+        for r in (1, 2, 3):
+            rep, bad = _compare(ranks[0][phase], ranks[r][phase], ref[phase], K, D, L, phase, False)
+            print(f"--- dp4 {config} {dtype} graph {phase} (ranks 0 and {r})")
+            print("\n".join(rep))
+            failures += [f"{phase} rank {r}: {b}" for b in bad]
+    assert not failures, failures
+
+
+@pytest.mark.timeout(900)
+def test_dp2_config3_per_rank_workload(cuda, tmp_path):
+    """BASELINE config 3's per-rank workload through the DP branch: two gloo ranks on the one GPU, each at B = 32,
+    T = 65,536, bf16, the step graph-captured (warm-up step, then two graphs around the exchange), against one
+    process on the concatenated B = 64 batch: code counts and the global reset rows bitwise, EMA sums rel 1e-6,
+    exchanged gradient rel 1e-5, replicas bitwise."""
+    config, dtype = "cfg2", "bf16"
+    cfg = W.CONFIGS[config]
+    K, D, L = cfg["num_embeddings"], cfg["latent_dim"], cfg["levels"]
+    ranks = _run_ranks("graph", tmp_path, config, dtype, batch=32, phases="step1")
+    old = W.B_LOCAL
+    W.B_LOCAL = 32
+    try:
+        m = W.build(64, config=config, dtype=dtype)
+        xs = W.batches(2, config)
+        m.train_step(xs[0])
+        torch.cuda.synchronize()
+        ref = W.snapshot(m)
+        del m
+        torch.cuda.empty_cache()
+    finally:
+        W.B_LOCAL = old
+    rep, bad = _compare(ranks[0]["step1"], ranks[1]["step1"], ref, K, D, L, "step1", True)
+    print("--- config 3 per-rank workload (B=32/rank, T=65536, bf16, graph)")
+    print("\n".join(rep))
+    assert not bad, bad
 
 
 @pytest.mark.timeout(600)
@@ -242,7 +313,8 @@ def test_bench_py_dp2_gloo_one_gpu(cuda):
     env = dict(os.environ, VQA_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch", "2", "--seq", "8192", "--no-cpu-baseline"]
+           "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch", "2", "--seq", "8192", "--no-cpu-baseline",
+           "--prior-batch", "1", "--prior-steps", "2"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -253,3 +325,8 @@ def test_bench_py_dp2_gloo_one_gpu(cuda):
     assert out["value"] > 0 and out["ms_per_step"] > 0
     want = 2 * 2 * 8192 / (out["ms_per_step"] * 1e-3)  # 2 ranks x batch 2 x 8192 frames per step
     assert abs(out["value"] - want) <= 1e-3 * want
+    # the config-4 leg through the same DP branch (the prior's bucket, two graphs around its exchange)
+    c4 = out["config4_prior_train"]
+    assert c4["n_gpus"] == 2 and c4["config"]["parallelism"] == "dp2" and c4["value"] > 0
+    assert abs(c4["value"] - 2 * 1 * 8192 * 2 / (c4["ms_per_step"] * 1e-3 * 2)) <= 1e-3 * c4["value"]
+    assert "config5_upsampler_decode" not in out  # rank 0 at N = 1 only

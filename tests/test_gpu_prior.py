@@ -360,6 +360,25 @@ def test_prior_test_step_and_metrics(cuda):
     assert float(pr.train_loss_tracker.result()) == 0.0
 
 
+def test_prior_evaluate_keras_semantics(cuda):
+    """Prior.evaluate (keras Model.evaluate, as src/callback/monitors.py:81 calls it on the validation dataset):
+    the trackers are reset, test_step runs on every batch (prior.py:337-372), and the running means over the
+    batches come back — as a dict, or flattened in keras order (tracker names first; these keys are not tracker
+    names, so sorted: accuracy, loss, perplexity)."""
+    pr, vals = _prior(CFG)
+    g = _gen(31)
+    batches = [torch.randint(0, CFG.bins - 1, (2, CFG.ctx), generator=g) for _ in range(3)]
+    want = [P.train_step_grads(P.to_torch(vals), CFG, c, torch.zeros(2, CFG.ctx, dtype=torch.bool))[:2] for c in batches]
+    pr.test_step(batches[2].cuda())  # stale tracker state that evaluate must reset
+    logs = pr.evaluate([b.cuda() for b in batches[:2]], return_dict=True)
+    mean_loss, mean_acc = (want[0][0] + want[1][0]) / 2, (want[0][1] + want[1][1]) / 2
+    assert abs(logs["loss"] - mean_loss) <= 1e-5 * mean_loss and abs(logs["accuracy"] - mean_acc) <= 1e-6
+    flat = pr.evaluate(torch.cat([b for b in batches[:2]]).cuda(), batch_size=2)
+    assert flat == [logs["accuracy"], logs["loss"], logs["perplexity(per word)"]]
+    one = pr.evaluate([b.cuda() for b in batches], steps=1, return_dict=True)
+    assert abs(one["loss"] - want[0][0]) <= 1e-5 * want[0][0]
+
+
 # ------------------------------------------------------------------ dropout, conditioning
 def test_dropout_mask_statistics_and_determinism(cuda):
     """keras Dropout(rate): kept elements scaled by 1/(1-rate), drop fraction = rate; counter-based mask:
@@ -618,7 +637,19 @@ def test_prior_checkpoint_resume_bitwise(cuda, tmp_path):
     assert torch.equal(a.optimizer.m, b.optimizer.m) and torch.equal(a.optimizer.v, b.optimizer.v)
     assert float(a.results()["loss"]) == float(b.results()["loss"])
     raw = torch.load(path, weights_only=True)
-    assert raw["format"] == "vqa-prior/1" and raw["iterations"] == 2
+    assert raw["format"] == "vqa-prior/2" and raw["iterations"] == 2
+    # a format-/1 file of the packed layout (the first releases) loads by name into the aligned layout
+    st = a.prior.store
+    pack = lambda flat: torch.cat([flat[o:o + int(np.prod(sh))] for _, (o, sh) in st.offsets.items()])  # noqa: E731
+    old = {k: v for k, v in raw.items() if k != "layout"}
+    old.update(format="vqa-prior/1", weights=pack(raw["weights"]), adam_m=pack(raw["adam_m"]), adam_v=pack(raw["adam_v"]))
+    assert old["weights"].numel() == st.count < st.size
+    torch.save(old, str(tmp_path / "prior_v1.pt"))
+    c = make(7)
+    c.load(str(tmp_path / "prior_v1.pt"))
+    d = make(8)
+    d.load(path)
+    assert torch.equal(c.prior.store.flat, d.prior.store.flat) and torch.equal(c.optimizer.v, d.optimizer.v)
 
 
 def test_train_step_small_prior_full_size(cuda):

@@ -392,7 +392,18 @@ def test_checkpoint_resume_bitwise(cuda, tmp_path, dtype):
     path = str(tmp_path / "ckpt.pt")
     a.save(path)
     ck = torch.load(path, weights_only=True)
-    assert ck["format"] == "vqa-vqvae/1" and int(ck["iterations"]) == 1
+    assert ck["format"] == "vqa-vqvae/2" and int(ck["iterations"]) == 1
+    # the same state written as a format-/1 file in the packed layout of the first releases (no gaps) loads by
+    # name into the aligned layout
+    st = a.store
+    pack = lambda flat: torch.cat([flat[o:o + int(np.prod(sh))] for _, (o, sh) in st.offsets.items()])  # noqa: E731
+    old = {k: v for k, v in ck.items() if k != "layout"}
+    old.update(format="vqa-vqvae/1", weights=pack(ck["weights"]), adam_m=pack(ck["adam_m"]), adam_v=pack(ck["adam_v"]))
+    torch.save(old, str(tmp_path / "ckpt_v1.pt"))
+    c = _model(cfg, B, dtype, R.init_params(cfg, 7), R.init_vq_state(cfg, 8))
+    c.load(str(tmp_path / "ckpt_v1.pt"))
+    torch.cuda.synchronize()
+    assert torch.equal(c.store.flat.cpu(), ck["weights"]) and torch.equal(c.optimizer.m.cpu(), ck["adam_m"])
     a.train_step(xs[1])
     ra = {k: float(v) for k, v in a.train_step(xs[2]).items()}
     b = _model(cfg, B, dtype, R.init_params(cfg, 5), R.init_vq_state(cfg, 6))  # different start, then load
@@ -408,6 +419,64 @@ def test_checkpoint_resume_bitwise(cuda, tmp_path, dtype):
         assert sa["calls"] == sb["calls"] == 3
     # the last step's metrics (b's trackers saw two steps, a's three: compare the last step's contribution)
     assert a.loss_slots.cpu().equal(b.loss_slots.cpu())
+
+
+def test_evaluate_keras_semantics(cuda):
+    """VQVAE.evaluate (keras Model.evaluate, as src/callback/vae_monitor.py:69 calls it on the validation dataset):
+    the model's trackers are reset, test_step (vqvae.py:148-172) runs on every batch — the codebook EMA included
+    (VectorQuantizer.py:75 defaults training=True) — and the running means come back. Against the fp64 oracle's
+    test_step sequence on the same two batches: loss keys rel 1e-5, codebook state after both batches (N_t on
+    >= 99 % of codes, m_t / E relative L2 1e-4; a row on a near-tie may take the other code)."""
+    c = CONFIGS["cfg1"]
+    cfg, B = c["cfg"], c["B"]
+    params, vq = R.init_params(cfg, 1), R.init_vq_state(cfg, 2)
+    xs = [R.synthetic_batch(B, cfg.input_len, seed=70 + i) for i in range(3)]
+    m = _model(cfg, B, "fp32", params, vq)
+    m.train_step(xs[2])  # tracker state that evaluate must reset; the oracle starts from the state after it
+    ref = R.RefVQVAE(cfg, params, vq, dtype=torch.float64)
+    _sync_oracle(ref, m)
+    logs = m.evaluate(xs[:2], return_dict=True)
+    outs = [ref.test_step(x) for x in xs[:2]]
+    for k in ("loss", "recon_loss", "vqvae_loss", "spectral_loss", "[0]level_loss", "[0]recon_loss", "[0]vq_loss",
+              "[0]spectral_loss"):
+        want = (outs[0][k] + outs[1][k]) / 2
+        assert abs(logs[k] - want) <= 1e-5 * abs(want), (k, logs[k], want)
+    st = m.get_vq_state()[0]
+    assert st["calls"] == ref.vq[0]["calls"] == 3
+    assert np.mean(np.isclose(st["N_t"], ref.vq[0]["N_t"].numpy(), rtol=1e-5, atol=0)) >= 0.99
+    for k in ("m_t", "embeddings"):
+        assert _l2(st[k], ref.vq[0][k].numpy()) < 1e-4, k
+    # flattened in keras order: tracker names first (model.metrics order), then the other keys sorted
+    flat = m.evaluate(np.concatenate(xs[:2]), batch_size=B)
+    names = [t.name for t in m.metrics]
+    order = [k for k in names if k in logs] + sorted(k for k in logs if k not in names)
+    assert len(flat) == len(logs) and order[0] == "spectral_loss"
+    assert m.evaluate(xs[:2], steps=1, return_dict=True).keys() == logs.keys()
+
+
+def test_compile_after_capture_uses_new_optimizer(cuda):
+    """Re-compiling after capture_train_step drops the captured step (it holds the old optimizer's m, v, step
+    counter and learning rate): the next train_step runs with the new optimizer, eagerly, and equals a model that
+    was compiled with it from the start."""
+    from vqa_optim import Adam
+    c = CONFIGS["cfg1"]
+    cfg, B = c["cfg"], c["B"]
+    params, vq = R.init_params(cfg, 1), R.init_vq_state(cfg, 2)
+    xs = [R.synthetic_batch(B, cfg.input_len, seed=80 + i) for i in range(2)]
+    a = _model(cfg, B, "fp32", params, vq)
+    a.capture_train_step(xs[0], warmup=1)
+    state = a.state_dict()
+    a.compile(Adam(learning_rate=5e-4))
+    assert a._graph is None
+    a.train_step(xs[1])
+    b = _model(cfg, B, "fp32", params, vq)
+    b.compile(Adam(learning_rate=5e-4))
+    b.store.flat.copy_(state["weights"].cuda())
+    b.set_vq_state(state["vq"])
+    b.train_step(xs[1])
+    torch.cuda.synchronize()
+    assert int(a.optimizer.iterations.item()) == 1
+    assert torch.equal(a.store.flat, b.store.flat)
 
 
 def test_repeated_step_bitwise(cuda):

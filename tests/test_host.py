@@ -158,3 +158,37 @@ def test_adam_rejects_host_callables():
     from vqa_optim import Adam
     with pytest.raises(TypeError):
         Adam(learning_rate=lambda step: 1e-3)
+
+
+def test_checkpoint_layouts_v1_packed_v1_aligned_v2():
+    """Checkpoint format /2 records each tensor's [offset, *shape]; a /1 file is read in the layout its length
+    identifies — the 16-byte-aligned one or the packed one of the first releases — and copied by name into the
+    aligned layout; anything else is rejected with a clear error."""
+    from vqa_layers import CKPT_VERSION, checkpoint_layout
+    st = ParamStore()
+    for n, s in (("a/bias", (1,)), ("b/kernel", (3, 1, 2)), ("c/bias", (5,)), ("d/kernel", (2, 2))):
+        st.add(n, s, "zeros")
+    assert st.count == 16 and st.size == 24  # offsets 0, 4, 12, 20
+    vals = {n: np.arange(int(np.prod(s)), dtype=np.float32).reshape(s) + 10 * i
+            for i, (n, s, _) in enumerate(st.specs)}
+    aligned = torch.zeros(st.size)
+    for n, (o, s) in st.offsets.items():
+        aligned[o:o + int(np.prod(s))] = torch.from_numpy(vals[n].reshape(-1))
+    packed = torch.cat([torch.from_numpy(vals[n].reshape(-1)) for n, _, _ in st.specs])
+    names = [n for n, _, _ in st.specs]
+    for flat in (aligned, packed):
+        ck = {"format": "vqa-vqvae/1", "param_names": names, "weights": flat}
+        lay = checkpoint_layout(ck, st, "vqvae", "x.pt")
+        assert torch.equal(st.from_layout(flat, lay, "x.pt"), aligned)
+    ck2 = {"format": f"vqa-vqvae/{CKPT_VERSION}", "layout": st.layout_record(), "weights": aligned}
+    assert torch.equal(st.from_layout(aligned, checkpoint_layout(ck2, st, "vqvae", "y.pt"), "y.pt"), aligned)
+    with pytest.raises(ValueError, match="fits neither"):
+        checkpoint_layout({"format": "vqa-vqvae/1", "param_names": names, "weights": torch.zeros(17)}, st, "vqvae", "z")
+    with pytest.raises(ValueError, match="differs"):
+        checkpoint_layout({"format": "vqa-vqvae/1", "param_names": names[::-1], "weights": packed}, st, "vqvae", "z")
+    with pytest.raises(ValueError, match="not a vqa-prior"):
+        checkpoint_layout(ck2, st, "prior", "z")
+    bad = st.layout_record()
+    bad["c/bias"] = [12, 4]
+    with pytest.raises(ValueError, match="shape"):
+        st.from_layout(aligned, bad, "w")

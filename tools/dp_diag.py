@@ -1,0 +1,167 @@
+"""DP exchange diagnosis (GPU dev tool): where does a wrong exchanged gradient come from?
+
+Two gloo ranks on cuda:0 run tests/dp_worker.py's sequence (cfg2_short, bf16, graph warm-up on a side stream)
+with `vqa_dp.exchange` replaced by an instrumented exchange over one of these paths:
+  device       dist.all_reduce on the DEVICE bucket (torch-gloo stages it through pinned host memory on a
+               high-priority pool stream behind an event on the current stream, copies the sum back there)
+  device_sync  the same after hipStreamSynchronize of the current stream (the round-3 intermediate fix)
+  host         the product path (vqa_dp.exchange: blocking copy out, CPU all_reduce, copy back)
+  emulate      the product path, preceded by an emulation of gloo's staging copy (event on the current
+               stream, high-priority stream waits, non_blocking D2H into pinned memory, stream sync)
+At the exchange each rank records, for the step's full bucket:
+  before   a device copy queued on the current stream at entry (what the collective must read)
+  staged   (emulate) the pinned copy the emulated staging read
+  after    a device copy queued on the current stream right after the exchange returns (the consumer's view:
+           what `_update` / the second graph reads), no host sync
+  final    the bucket after a device synchronize
+and the driver checks, per rank:  before == single-process local gradient,  staged == before,
+after == before0 + before1 (fp32 a+b is commutative, so bitwise),  final == after.
+A wrong `after` with a right `final` = consumer ordering; a wrong `final` equal to `after` = a wrong sum
+(the staging read the wrong bytes); `final` != `after` = a write after the exchange.
+
+    python tools/dp_diag.py PATH REPS [MODE]
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"), ROOT, os.path.join(ROOT, "tests")]
+
+import torch  # noqa: E402
+
+import dp_worker as W  # noqa: E402
+
+CONFIG, DTYPE = "cfg2_short", "bf16"
+
+
+def worker(path, mode, out):
+    import torch.distributed as dist
+    import vqa_dp
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = W.build(W.B_LOCAL, config=CONFIG, dtype=DTYPE)
+    xs = [x[rank * W.B_LOCAL:(rank + 1) * W.B_LOCAL] for x in W.batches(world, CONFIG)]
+    P = m.layout["grads"][1]
+    rec = []
+    orig = vqa_dp.exchange
+
+    def diag(bucket, group=None):
+        if bucket.numel() <= P or rec:  # instrument the first full-bucket exchange only
+            return orig(bucket, group)
+        cur = torch.cuda.current_stream()
+        r = {"before": bucket.detach().clone()}
+        if path == "device":
+            dist.all_reduce(bucket, group=group)
+        elif path == "device_sync":
+            cur.synchronize()
+            dist.all_reduce(bucket, group=group)
+        else:
+            if path == "emulate":
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                side = torch.cuda.Stream(priority=-1)
+                side.wait_event(ev)
+                staged = torch.empty(bucket.shape, dtype=bucket.dtype, pin_memory=True)
+                with torch.cuda.stream(side):
+                    staged.copy_(bucket, non_blocking=True)
+                side.synchronize()
+                r["staged"] = staged.clone()
+            orig(bucket, group)
+        r["after"] = bucket.detach().clone()
+        torch.cuda.synchronize()
+        r["final"] = bucket.detach().cpu().clone()
+        r["before"], r["after"] = r["before"].cpu(), r["after"].cpu()
+        rec.append(r)
+        return world
+
+    vqa_dp.exchange = diag
+    res = W.run(m, xs, mode)
+    r = rec[0]
+    r["step1"] = torch.cat([res["step1"]["grads"], res["step1"]["stats"]])
+    r["P"] = P
+    r["offsets"] = {k: (int(o), int(torch.Size(sh).numel())) for k, (o, sh) in m.store.offsets.items()}
+    torch.save(r, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def reference():
+    refs = []
+    for r in range(2):
+        m = W.build(W.B_LOCAL, config=CONFIG, dtype=DTYPE)
+        x = m._as_input(W.batches(2, CONFIG)[0][r * W.B_LOCAL:(r + 1) * W.B_LOCAL])
+        m._compute(x, True)
+        torch.cuda.synchronize()
+        refs.append(m.bucket.detach().cpu().clone())
+        del m
+    torch.cuda.empty_cache()
+    return refs
+
+
+def where(d, offsets, P):
+    per = sorted(((float(d[o:o + k].max()), int((d[o:o + k] > 0).sum()), name) for name, (o, k) in offsets.items()),
+                 reverse=True)
+    per = [f"{nm} {v:.1e}/{c}" for v, c, nm in per if v > 0][:6]
+    if float(d[P:].max()) > 0:
+        per.append(f"stats/losses {float(d[P:].max()):.1e}/{int((d[P:] > 0).sum())}")
+    return per
+
+
+def main():
+    path, reps = sys.argv[1], int(sys.argv[2])
+    mode = sys.argv[3] if len(sys.argv) > 3 else "graph"
+    refs = reference()
+    out_dir = os.path.join(ROOT, "gpurun_out", "dp_diag")
+    os.makedirs(out_dir, exist_ok=True)
+    summary = []
+    for rep in range(reps):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        procs, outs = [], []
+        for r in range(2):
+            out = os.path.join(out_dir, f"{path}_{mode}_rank{r}.pt")
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, __file__, "--worker", path, mode, out], env=env))
+            outs.append(out)
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+        rr = [torch.load(o, weights_only=True) for o in outs]
+        P = rr[0]["P"]
+        want = rr[0]["before"] + rr[1]["before"]
+        line = {"path": path, "mode": mode, "rep": rep}
+        for r in range(2):
+            g = rr[r]
+            n_loc = int((g["before"][:P] != refs[r][:P]).sum())
+            chk = {"before!=local": n_loc,
+                   "after!=sum": int((g["after"] != want).sum()),
+                   "final!=sum": int((g["final"] != want).sum()),
+                   "final!=after": int((g["final"] != g["after"]).sum()),
+                   "step1!=final": int((g["step1"] != g["final"]).sum())}
+            if "staged" in g:
+                chk["staged!=before"] = int((g["staged"] != g["before"]).sum())
+            if chk["after!=sum"]:
+                d = (g["after"].double() - want.double()).abs()
+                chk["after_where"] = where(d, g["offsets"], P)
+                bad = d > 0
+                # is the wrong value this rank's own local value (the other's missing), or the other's?
+                chk["after==own_before"] = int((g["after"][bad] == g["before"][bad]).sum())
+                chk["after==other_before"] = int((g["after"][bad] == rr[1 - r]["before"][bad]).sum())
+            line[f"rank{r}"] = chk
+        print(json.dumps(line), flush=True)
+        summary.append(line)
+    nbad = sum(1 for ln in summary if any(ln[f"rank{r}"]["after!=sum"] or ln[f"rank{r}"]["final!=sum"]
+                                          for r in range(2)))
+    print(f"SUMMARY path={path} mode={mode}: {nbad} of {reps} runs with a wrong exchanged bucket", flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--worker":
+        worker(sys.argv[2], sys.argv[3], sys.argv[4])
+    else:
+        main()

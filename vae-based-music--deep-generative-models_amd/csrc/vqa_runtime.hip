@@ -159,7 +159,8 @@ static int blocks_for(long long n, int cap) {
 using namespace vqa;
 
 extern "C" const char* vqa_get_last_error(void) { return g_err; }
-extern "C" const char* vqa_version(void) { return "libvqa 0.1 gfx950"; }
+extern "C" const char* vqa_version(void) { return "libvqa 0.2 gfx950 abi 2"; }
+extern "C" int vqa_abi_version(void) { return VQA_ABI_VERSION; }
 
 extern "C" size_t vqa_mse_loss_workspace(int64_t n) { return n < 1 ? 0 : (size_t)blocks_for(n, 1024) * sizeof(float); }
 

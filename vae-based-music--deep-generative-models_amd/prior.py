@@ -33,8 +33,9 @@ import torch
 import vqa_dp
 import vqa_lib as V
 from conditioners import ConditionerNet
-from vqa_layers import ParamStore
+from vqa_layers import CKPT_VERSION, ParamStore, checkpoint_layout
 from vqa_metrics import Mean
+from vqa_module import keras_evaluate
 from vqa_optim import Adam
 
 
@@ -777,6 +778,13 @@ class Prior:
         self.train_accuracy_tracker.update_state(out[1])
         return self.results()
 
+    def evaluate(self, x=None, y=None, batch_size=None, verbose=0, steps=None, return_dict=False, **kwargs):
+        """keras Model.evaluate over test_step (prior.py:337-372), as src/callback/monitors.py:81 calls it on the
+        validation dataset: the loss / accuracy trackers reset, test_step per batch, their running means returned
+        (vqa_module.keras_evaluate)."""
+        return keras_evaluate(self, x, y, batch_size=batch_size, verbose=verbose, steps=steps,
+                              return_dict=return_dict)
+
     def capture_train_step(self, codes_example, teacher_force_rate=0.2, warmup=1):
         """Record the whole step (both passes, the conditioner, backward, Adam, metrics) as one hipGraph — two
         around the eager all_reduce under data parallelism; later train_step calls with the same shapes copy the
@@ -817,7 +825,8 @@ class Prior:
         also drives teacher forcing and dropout), and the loss / accuracy trackers: resuming reproduces the
         uninterrupted run bit for bit."""
         st = self.prior.store
-        out = {"format": "vqa-prior/1", "param_names": [n for n, _, _ in st.specs],
+        out = {"format": f"vqa-prior/{CKPT_VERSION}", "param_names": [n for n, _, _ in st.specs],
+               "layout": st.layout_record(),
                "config": {"level": self.level, "bins": self.bins, "context_length": self.context_length,
                           "width": self.prior.d_model, "depth": self.prior.depth, "heads": self.prior.heads,
                           "blocks": self.prior.blocks, "genre_classes": self.genre_bins},
@@ -828,16 +837,14 @@ class Prior:
         torch.save(out, path)
 
     def load(self, path: str):
-        """Restore a `save` checkpoint (loaded weights-only: nothing in the file is executed)."""
+        """Restore a `save` checkpoint (loaded weights-only: nothing in the file is executed); format /2 is
+        copied tensor by tensor through its recorded layout, /1 in the layout its length identifies."""
         ck = torch.load(path, map_location="cpu", weights_only=True)
         st = self.prior.store
-        if ck.get("format") != "vqa-prior/1":
-            raise ValueError(f"{path}: not a vqa-prior/1 checkpoint")
-        if ck["param_names"] != [n for n, _, _ in st.specs]:
-            raise ValueError(f"{path}: parameter layout differs from this prior's")
-        st.flat.copy_(ck["weights"].to(self.device))
-        self.optimizer.m.copy_(ck["adam_m"].to(self.device))
-        self.optimizer.v.copy_(ck["adam_v"].to(self.device))
+        lay = checkpoint_layout(ck, st, "prior", path)
+        st.flat.copy_(st.from_layout(ck["weights"], lay, path).to(self.device))
+        self.optimizer.m.copy_(st.from_layout(ck["adam_m"], lay, f"{path} (adam_m)").to(self.device))
+        self.optimizer.v.copy_(st.from_layout(ck["adam_v"], lay, f"{path} (adam_v)").to(self.device))
         self.optimizer.iterations.fill_(int(ck["iterations"]))
         self._step = int(ck["step"])
         for t, acc in zip(self.metrics, ck["trackers"]):

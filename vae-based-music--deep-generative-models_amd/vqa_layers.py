@@ -107,6 +107,57 @@ class ParamStore:
         host = self.grad[:self.size].detach().cpu().numpy()
         return {n: host[o:o + int(np.prod(s))].reshape(s).copy() for n, (o, s) in self.offsets.items()}
 
+    # ---- checkpoint layout (format /2 saves it; /1 files are read by their length)
+    def layout_record(self) -> Dict[str, List[int]]:
+        """name -> [offset, *shape] of the flat buffers (weights, Adam m and v share it)."""
+        return {n: [int(o), *map(int, s)] for n, (o, s) in self.offsets.items()}
+
+    def legacy_layout(self, flat_len: int, what: str) -> Dict[str, List[int]]:
+        """The layout a format-/1 checkpoint of this model was written in, told apart by its length: the
+        16-byte-aligned layout (`size` floats) or the packed one of the first releases (`count` floats, every
+        tensor right after the previous one). Anything else is rejected."""
+        if flat_len == self.size:
+            return self.layout_record()
+        if flat_len == self.count:
+            out, off = {}, 0
+            for n, shape, _ in self.specs:
+                out[n] = [off, *shape]
+                off += int(np.prod(shape))
+            return out
+        raise ValueError(f"{what}: a flat buffer of {flat_len} floats fits neither this model's aligned layout "
+                         f"({self.size}) nor its packed layout ({self.count})")
+
+    def from_layout(self, flat: torch.Tensor, layout: Dict[str, List[int]], what: str) -> torch.Tensor:
+        """Copy a saved flat buffer, tensor by tensor, into this store's layout (gaps zero) -> CPU fp32."""
+        if set(layout) != set(self.offsets):
+            raise ValueError(f"{what}: parameter names differ from this model's")
+        flat = flat.detach().to("cpu", torch.float32).reshape(-1)
+        out = torch.zeros(self.size, dtype=torch.float32)
+        for n, (off, shape) in self.offsets.items():
+            rec = layout[n]
+            if tuple(rec[1:]) != tuple(shape):
+                raise ValueError(f"{what}: {n} has shape {tuple(rec[1:])}, this model {tuple(shape)}")
+            k = int(np.prod(shape))
+            if rec[0] < 0 or rec[0] + k > flat.numel():
+                raise ValueError(f"{what}: {n} lies outside the saved buffer")
+            out[off:off + k] = flat[rec[0]:rec[0] + k]
+        return out
+
+
+CKPT_VERSION = 2
+
+
+def checkpoint_layout(ck: dict, store: ParamStore, family: str, path: str) -> Dict[str, List[int]]:
+    """The saved layout of a 'vqa-<family>/1' or '/2' checkpoint (see ParamStore.legacy_layout)."""
+    fmt = ck.get("format")
+    if fmt == f"vqa-{family}/{CKPT_VERSION}":
+        return {n: list(v) for n, v in ck["layout"].items()}
+    if fmt == f"vqa-{family}/1":
+        if ck["param_names"] != [n for n, _, _ in store.specs]:
+            raise ValueError(f"{path}: parameter layout differs from this model's")
+        return store.legacy_layout(int(ck["weights"].numel()), path)
+    raise ValueError(f"{path}: not a vqa-{family}/1 or /{CKPT_VERSION} checkpoint (format {fmt!r})")
+
 
 def _flags_for(x: torch.Tensor, y_dtype: torch.dtype, cdt: torch.dtype) -> int:
     f = 0

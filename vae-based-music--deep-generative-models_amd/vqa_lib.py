@@ -18,8 +18,10 @@ LIB_PATH = os.path.join(HERE, "libvqa.so")
 F32, BF16 = 0, 1
 PRE_RELU, ADD_RESIDUAL, POST_MASK, X_F32, Y_F32 = 1, 2, 4, 8, 16
 
+ABI_VERSION = 2  # include/vqa.h VQA_ABI_VERSION this binding is written against
+
 EXPORTED = [
-    "vqa_get_last_error", "vqa_version", "vqa_same_pad_left", "vqa_same_out_len",
+    "vqa_get_last_error", "vqa_version", "vqa_abi_version", "vqa_same_pad_left", "vqa_same_out_len",
     "vqa_conv1d_fwd", "vqa_conv1d_bwd_data", "vqa_conv1d_bwd_weight", "vqa_conv1d_bwd_weight_workspace",
     "vqa_conv1d_transpose_fwd", "vqa_conv1d_transpose_bwd_data", "vqa_conv1d_transpose_bwd_weight",
     "vqa_conv1d_transpose_bwd_weight_workspace",
@@ -61,6 +63,7 @@ _CONVT = [_I] * 10  # B T_in T_out C_in C_out K stride pad flags dtype
 _SIGS = {
     "vqa_get_last_error": (ctypes.c_char_p, []),
     "vqa_version": (ctypes.c_char_p, []),
+    "vqa_abi_version": (_I, []),
     "vqa_same_pad_left": (_I, [_I, _I, _I, _I]),
     "vqa_same_out_len": (_I, [_I, _I]),
     "vqa_conv1d_fwd": (_I, [_P, _P, _P, _P, _P] + _CONV + [_P]),
@@ -150,6 +153,10 @@ def lib() -> ctypes.CDLL:
             raise ImportError(f"libvqa.so not found at {LIB_PATH}; build it with `python -c "
                               f"'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
         L = ctypes.CDLL(LIB_PATH)
+        abi = L.vqa_abi_version() if hasattr(L, "vqa_abi_version") else 1
+        if abi != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} implements C-ABI revision {abi}, this binding needs {ABI_VERSION}: "
+                              f"rebuild the library (argument lists differ between revisions)")
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 from typing import Optional
 
+import numpy as np
 import torch
 
 from vqa_layers import ParamStore
@@ -51,3 +52,50 @@ class Layer:
 
     def _param_names(self):
         return []
+
+
+def _is_array(a) -> bool:
+    return isinstance(a, (torch.Tensor, np.ndarray))
+
+
+def keras_evaluate(model, x=None, y=None, batch_size=None, verbose=0, steps=None, return_dict=False):
+    """keras Model.evaluate (TF 2.7 semantics) over `model.test_step`, as the reference's monitors call it
+    (src/callback/vae_monitor.py:69, src/callback/monitors.py:81: `self.model.evaluate(self.val_dataset)`):
+      - the model's metrics are reset first (`model.reset_metrics()`), then `test_step` runs on every batch —
+        for the VQ-VAE that includes the codebook EMA update (VectorQuantizer.py:75 defaults training=True);
+      - `x` is a dataset-like iterable of batches (each a tensor / array or a tuple (x, y, ...), as tf.data
+        yields them), or an array (optionally with `y`) cut into `batch_size` rows (default 32, the last batch
+        partial); `steps` caps the number of batches;
+      - returns the last step's logs (the trackers' running means) as a dict of floats with `return_dict`,
+        otherwise keras' flatten_metrics_in_order: the values whose keys are tracker names first, in
+        `model.metrics` order, then the other keys sorted; a single value is returned bare."""
+    if x is None:
+        raise ValueError("evaluate needs data")
+    if isinstance(x, tuple) and len(x) == 2 and _is_array(x[0]) and y is None:
+        x, y = x
+    if _is_array(x):
+        n = int(x.shape[0])
+        bs = int(batch_size or 32)
+        if y is not None and int(y.shape[0]) != n:
+            raise ValueError(f"x has {n} rows, y {int(y.shape[0])}")
+        batches = ((x[i:i + bs], y[i:i + bs]) if y is not None else x[i:i + bs] for i in range(0, n, bs))
+    else:
+        if y is not None:
+            raise ValueError("`y` is only accepted with array inputs (a dataset yields (x, y) batches itself)")
+        batches = iter(x)
+    model.reset_metrics()
+    logs = None
+    for i, batch in enumerate(batches):
+        if steps is not None and i >= steps:
+            break
+        logs = model.test_step(batch)
+        if verbose:
+            print(f"evaluate batch {i + 1}", {k: round(float(v), 6) for k, v in logs.items()})
+    if logs is None:
+        raise ValueError("evaluate got no batches")
+    logs = {k: float(v) for k, v in logs.items()}
+    if return_dict:
+        return logs
+    names = [m.name for m in model.metrics]
+    out = [logs[k] for k in names if k in logs] + [logs[k] for k in sorted(logs) if k not in names]
+    return out[0] if len(out) == 1 else out

@@ -30,8 +30,9 @@ import vqa_dp
 import vqa_lib as V
 from data_utils import SpectralTarget, multispectral_loss_and_grad
 from encdec import Decoder, Encoder
-from vqa_layers import ParamStore
+from vqa_layers import CKPT_VERSION, ParamStore, checkpoint_layout
 from vqa_metrics import SlotMean
+from vqa_module import keras_evaluate
 from vqa_optim import Adam
 from VectorQuantizer import VectorQuantizer
 
@@ -182,8 +183,12 @@ class VQVAE:
 
     # ------------------------------------------------------------------ keras-like API
     def compile(self, optimizer=None, **kwargs):
+        """keras Model.compile: a vqa_optim.Adam (float or LearningRateSchedule learning rate). A captured step
+        is dropped: it holds the previous optimizer's buffers (m, v, step counter, learning rate)."""
         self.optimizer = optimizer or Adam()
         self.optimizer.build(self.store)
+        self._graph = None
+        self._graph_pool = None
 
     @property
     def metrics(self):
@@ -338,6 +343,13 @@ class VQVAE:
             self._exchange(grads=False)
             self._update(apply_grads=False)
         return self.results()
+
+    def evaluate(self, x=None, y=None, batch_size=None, verbose=0, steps=None, return_dict=False, **kwargs):
+        """keras Model.evaluate over test_step (vqvae.py:148-172), as src/callback/vae_monitor.py:69 calls it on
+        the validation dataset: metrics reset, test_step per batch (the codebook EMA runs, VectorQuantizer.py:75),
+        the running means returned (vqa_module.keras_evaluate)."""
+        return keras_evaluate(self, x, y, batch_size=batch_size, verbose=verbose, steps=steps,
+                              return_dict=return_dict)
 
     # ------------------------------------------------------------------ hipGraph capture
     def capture_train_step(self, x_example, warmup: int = 2):
@@ -495,7 +507,8 @@ class VQVAE:
         level's codebook E, m_t, N_t and reset counter: resuming reproduces the uninterrupted run bit for
         bit (every reduction of the step runs in a fixed order)."""
         sd = self.state_dict()
-        out = {"format": "vqa-vqvae/1", "param_names": [n for n, _, _ in self.store.specs],
+        out = {"format": f"vqa-vqvae/{CKPT_VERSION}", "param_names": [n for n, _, _ in self.store.specs],
+               "layout": self.store.layout_record(),
                "config": {"input_shape": list(self.input_shape), "levels": self.levels,
                           "latent_dim": self.latent_dim, "num_embeddings": self.num_embeddings,
                           "down_depth": list(self.down_depth), "strides": list(self.strides)},
@@ -510,17 +523,21 @@ class VQVAE:
         torch.save(out, path)
 
     def load(self, path: str):
-        """Restore a `save` checkpoint (loaded weights-only: nothing in the file is executed)."""
+        """Restore a `save` checkpoint (loaded weights-only: nothing in the file is executed). Format /2 records
+        each tensor's offset, and the weights and Adam moments are copied tensor by tensor into this model's
+        layout; a /1 file is read in the layout its length identifies (aligned or the earlier packed one)."""
         ck = torch.load(path, map_location="cpu", weights_only=True)
-        if ck.get("format") != "vqa-vqvae/1":
-            raise ValueError(f"{path}: not a vqa-vqvae/1 checkpoint")
-        if ck["param_names"] != [n for n, _, _ in self.store.specs]:
-            raise ValueError(f"{path}: parameter layout differs from this model's")
-        sd = {"weights": ck["weights"], "vq": [{k: ck[f"vq{l}/{k}"].numpy() for k in ("embeddings", "m_t", "N_t")}
-                                               | {"calls": ck[f"vq{l}/calls"]} for l in range(self.levels)]}
-        for k in ("adam_m", "adam_v", "iterations"):
+        lay = checkpoint_layout(ck, self.store, "vqvae", path)
+        if ck.get("config", {}).get("levels", self.levels) != self.levels:
+            raise ValueError(f"{path}: {ck['config']['levels']} levels, this model {self.levels}")
+        sd = {"weights": self.store.from_layout(ck["weights"], lay, path),
+              "vq": [{k: ck[f"vq{l}/{k}"].numpy() for k in ("embeddings", "m_t", "N_t")}
+                     | {"calls": ck[f"vq{l}/calls"]} for l in range(self.levels)]}
+        for k in ("adam_m", "adam_v"):
             if k in ck:
-                sd[k] = ck[k]
+                sd[k] = self.store.from_layout(ck[k], lay, f"{path} ({k})")
+        if "iterations" in ck:
+            sd["iterations"] = ck["iterations"]
         self.load_state_dict(sd)
 
     def load_state_dict(self, sd):
