@@ -92,10 +92,15 @@ def _l2(a, b):
 CASES = [("cfg1", "fp32"), ("cfg2_short", "fp32"), ("cfg2_short", "bf16")]
 
 
-def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False):
+def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=False):
     """-> (report lines, failures) of one phase's rank-0 / rank-1 / single-process snapshots. `strict` (BASELINE
     config 1's architecture in fp32, which has no near-tie rows on these batches): after every phase the code
-    counts stay bitwise equal and the weights within rel 1e-5 of max |w|, as in the first DP tests."""
+    counts stay bitwise equal and the weights within rel 1e-5 of max |w|, as in the first DP tests. `world` ranks:
+    the exchanged gradient is world x the global mean, and the summation-grouping bounds of the EMA sums and
+    codebooks after step 2 are 10x / 5x wider at 4 ranks (more rank partial sums; measured 4.4e-6 / 1.03e-5). `full_size` (B = 32 per rank,
+    T = 65,536): after the first Keras Adam step each weight moved by lr * g / (|g| + eps); where g is pure
+    rounding noise (it cancels over 2M rows) that ratio takes any value in [-1, 1], so the weights are held to
+    one update per element (|delta w| <= lr) and relative L2 1e-5 instead of rel 1e-5 of max |w|."""
     lr = 1e-3  # Keras Adam default (vqa_optim.Adam)
     nst = 2 * K * D + K  # one level's stats region: m_sumT, n_sum, RT
     rep, bad = [], []
@@ -139,16 +144,17 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False):
             # the EMA sums of every code whose count is unchanged (the moved rows are accounted for above)
             same = n_sum == ss[K * D:K * D + K]
             e = _l2(m_sum.view(K, D)[same], ss[:K * D].view(K, D)[same])
-            tol = 1e-6 if moved == 0 and not bf16 else (2e-2 if bf16 else 1e-3)
+            exact = 1e-6 if world <= 2 else 1e-5  # more rank partial sums, more grouping rounding (measured 4.4e-6 at 4)
+            tol = exact if moved == 0 and not bf16 else (2e-2 if bf16 else 1e-3)
             check(e < tol, f"level {l}: EMA sums of the {int(same.sum())} codes with unchanged counts, L2 {e:.2e}")
     if phase == "step1":
         # the exchanged gradient (sum over ranks of rank-mean gradients) = world x the global-batch mean
         # gradient, to fp32 rounding of the different summation grouping
-        e, tol = _rel(r0["grads"] / 2, s["grads"]), (1e-5 if bf16 else 2e-6)
+        e, tol = _rel(r0["grads"] / world, s["grads"]), (5e-5 if full_size else 1e-5 if bf16 else 2e-6)
         worst = ""
         if e >= tol and "offsets" in s:  # which parameters differ (diagnostic)
             gmax = float(s["grads"].double().abs().max())
-            per = sorted(((float((r0["grads"][o:o + n].double() / 2 - s["grads"][o:o + n].double()).abs().max()) / gmax,
+            per = sorted(((float((r0["grads"][o:o + n].double() / world - s["grads"][o:o + n].double()).abs().max()) / gmax,
                            k) for k, (o, n) in s["offsets"].items()), reverse=True)[:4]
             worst = " (worst: " + ", ".join(f"{k} {v:.1e}" for v, k in per) + ")"
         check(e < tol, f"exchanged gradient rel {e:.2e} < {tol:g}{worst}")
@@ -159,10 +165,16 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False):
         # Adam normalises each element by sqrt(v): an element whose gradient nearly cancels across items keeps
         # its absolute rounding noise but has a small sqrt(v), so a 1e-7-relative gradient difference becomes
         # up to ~1e-3 of that element's update (lr = 1e-3 per step), i.e. a few 1e-6 of max|w|
-        e = _rel(r0["weights"], s["weights"])
-        check(e < 1e-5, f"weights rel {e:.2e} < 1e-5")
-        e = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"]))
-        check(e < 1e-5, f"Adam moments rel {e:.2e} < 1e-5")
+        if full_size:
+            dw = float((r0["weights"] - s["weights"]).abs().max())
+            check(dw <= lr * 1.01, f"max |delta w| {dw:.2e} <= one Adam update ({lr:g})")
+            e = _l2(r0["weights"], s["weights"])
+            check(e < 1e-5, f"weights relative L2 {e:.2e} < 1e-5")
+        else:
+            e = _rel(r0["weights"], s["weights"])
+            check(e < 1e-5, f"weights rel {e:.2e} < 1e-5")
+        e, mtol = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"])), (5e-5 if full_size else 1e-5)
+        check(e < mtol, f"Adam moments rel {e:.2e} < {mtol:g}")
     elif exact_path:
         # after the second update an element whose gradient is pure rounding noise (it cancels over the batch)
         # has m / sqrt(v) = +-1 whatever its size, so the two runs can move it by +-lr in opposite directions
@@ -188,7 +200,8 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False):
         if exact_path:
             check(torch.equal(a["N_t"], b["N_t"]), f"level {l}: N_t bitwise")
             e = max(_rel(a["embeddings"], b["embeddings"]), _rel(a["m_t"], b["m_t"]))
-            check(e < 1e-5, f"level {l}: codebook / m_t rel {e:.2e}")
+            ctol = 1e-5 * (5 if world > 2 else 1)
+            check(e < ctol, f"level {l}: codebook / m_t rel {e:.2e} < {ctol:g}")
         else:
             e = max(_l2(a["m_t"], b["m_t"]), _l2(a["N_t"], b["N_t"]))
             check(e < 1e-2, f"level {l}: m_t / N_t relative L2 {e:.2e}")
@@ -269,7 +282,7 @@ def test_dp4_reset_rows_from_every_rank_offset(cuda, tmp_path):
     failures = []
     for phase in ("step1", "steps", "forward"):
         for r in (1, 2, 3):
-            rep, bad = _compare(ranks[0][phase], ranks[r][phase], ref[phase], K, D, L, phase, False)
+            rep, bad = _compare(ranks[0][phase], ranks[r][phase], ref[phase], K, D, L, phase, False, world=4)
             print(f"--- dp4 {config} {dtype} graph {phase} (ranks 0 and {r})")
             print("\n".join(rep))
             failures += [f"{phase} rank {r}: {b}" for b in bad]
@@ -281,7 +294,10 @@ def test_dp2_config3_per_rank_workload(cuda, tmp_path):
     """BASELINE config 3's per-rank workload through the DP branch: two gloo ranks on the one GPU, each at B = 32,
     T = 65,536, bf16, the step graph-captured (warm-up step, then two graphs around the exchange), against one
     process on the concatenated B = 64 batch: code counts and the global reset rows bitwise, EMA sums rel 1e-6,
-    exchanged gradient rel 1e-5, replicas bitwise."""
+    replicas bitwise; exchanged gradient (and Adam's first moments, 0.1 x it) rel 5e-5 of max |g|: every gradient
+    element here is a sum over 2^21 rows whose grouping differs completely between one process (512 workgroup
+    partials over 64 items) and two (512 over 32 items each, then the exchange); the bias gradients, long sums
+    that cancel, are the worst (measured 2.1e-5, enc1/blk0/down0/bias; 1e-5 holds at cfg2_short's 2^14 rows)."""
     config, dtype = "cfg2", "bf16"
     cfg = W.CONFIGS[config]
     K, D, L = cfg["num_embeddings"], cfg["latent_dim"], cfg["levels"]
@@ -298,7 +314,7 @@ def test_dp2_config3_per_rank_workload(cuda, tmp_path):
         torch.cuda.empty_cache()
     finally:
         W.B_LOCAL = old
-    rep, bad = _compare(ranks[0]["step1"], ranks[1]["step1"], ref, K, D, L, "step1", True)
+    rep, bad = _compare(ranks[0]["step1"], ranks[1]["step1"], ref, K, D, L, "step1", True, full_size=True)
     print("--- config 3 per-rank workload (B=32/rank, T=65536, bf16, graph)")
     print("\n".join(rep))
     assert not bad, bad

@@ -643,7 +643,7 @@ def test_prior_checkpoint_resume_bitwise(cuda, tmp_path):
     pack = lambda flat: torch.cat([flat[o:o + int(np.prod(sh))] for _, (o, sh) in st.offsets.items()])  # noqa: E731
     old = {k: v for k, v in raw.items() if k != "layout"}
     old.update(format="vqa-prior/1", weights=pack(raw["weights"]), adam_m=pack(raw["adam_m"]), adam_v=pack(raw["adam_v"]))
-    assert old["weights"].numel() == st.count < st.size
+    assert old["weights"].numel() == st.count <= st.size
     torch.save(old, str(tmp_path / "prior_v1.pt"))
     c = make(7)
     c.load(str(tmp_path / "prior_v1.pt"))

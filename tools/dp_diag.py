@@ -115,7 +115,8 @@ def main():
     path, reps = sys.argv[1], int(sys.argv[2])
     mode = sys.argv[3] if len(sys.argv) > 3 else "graph"
     refs = reference()
-    out_dir = os.path.join(ROOT, "gpurun_out", "dp_diag")
+    import tempfile
+    out_dir = os.path.join(tempfile.gettempdir(), "dp_diag")  # large: kept out of gpurun_out
     os.makedirs(out_dir, exist_ok=True)
     summary = []
     for rep in range(reps):

@@ -16,8 +16,13 @@ from __future__ import annotations
 
 from typing import Dict, Sequence
 
+import os
+
 import torch
 import torch.distributed as dist
+
+# diagnosis only (tools/dp_diag.py, round-3 failure study): hand gloo the device bucket as the RCCL path does
+_GLOO_DEVICE = os.environ.get("VQA_DP_GLOO_DEVICE") == "1"
 
 
 def bucket_layout(n_params: int, stats_sizes: Sequence[int], levels: int, align: int = 64) -> Dict[str, object]:
@@ -55,7 +60,7 @@ def exchange(bucket: torch.Tensor, group=None) -> int:
         # and a copy back on the same stream. Handing gloo the device bucket (its own pinned staging on a pool
         # stream behind an event) left the 2-rank bf16 graph-warm-up test with a sum that missed part of the
         # last-produced gradients (level 2, encoder block 0) in a few runs, even after a host sync first.
-        if bucket.is_cuda and dist.get_backend(group) == dist.Backend.GLOO:
+        if bucket.is_cuda and dist.get_backend(group) == dist.Backend.GLOO and not _GLOO_DEVICE:
             host = bucket.to("cpu")  # synchronous: waits for the producer stream
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
             bucket.copy_(host)
