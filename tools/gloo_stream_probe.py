@@ -9,6 +9,9 @@ everything has finished. Cases:
               levels' streams join the producer stream
   side_sync   like side, with hipStreamSynchronize of the current stream before the all_reduce
   side_host   like side, through the product's vqa_dp.exchange (host staging on the current stream)
+  side_join3  the step's topology: three producer streams (the levels), each writing its third of the tensor
+              behind a spin of a different length, all joined into the side stream; more streams than the
+              box's 4 hardware queues are alive (the levels', the side stream, gloo's pool stream, the default)
 Prints one line per case: the sum (want 2 * world... = 3.0 with values 1 and 2) and the stale value if the
 staging copy ran before the producer finished.
 
@@ -32,14 +35,25 @@ def run(rank, world, port, cycles, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import vqa_dp
     out = {}
-    for case in ("default", "side", "side_join", "side_sync", "side_host", "default", "side"):
+    levels = [torch.cuda.Stream() for _ in range(3)]
+    for case in ("default", "side", "side_join", "side_sync", "side_host", "side_join3", "side_join3", "default",
+                 "side"):
         t = torch.zeros(1 << 20, device="cuda")  # 4 MB, stale value 0
         torch.cuda.synchronize()
         dist.barrier()
         s = torch.cuda.Stream() if case != "default" else torch.cuda.current_stream()
         other = torch.cuda.Stream()
         with torch.cuda.stream(s):
-            if case == "side_join":
+            if case == "side_join3":
+                n3 = t.numel() // 3
+                for i, ls in enumerate(levels):
+                    ls.wait_stream(s)
+                    with torch.cuda.stream(ls):
+                        torch.cuda._sleep(cycles // (3 - i))
+                        t[i * n3:(i + 1) * n3 if i < 2 else t.numel()].fill_(rank + 1.0)
+                for ls in levels:
+                    s.wait_stream(ls)
+            elif case == "side_join":
                 other.wait_stream(s)
                 with torch.cuda.stream(other):
                     torch.cuda._sleep(cycles)

@@ -1235,26 +1235,26 @@ __device__ __forceinline__ float reduce_col16(const float* ws, int nparts, int E
   return t;
 }
 
-// 16-byte form for rows whose length and base keep float4 alignment: block = 64 elements (16 lanes x 4) x 16
-// part groups, so each wave reads 256 contiguous bytes of 4 rows per load. Fixed order as above.
-constexpr int kRedCols4 = 64;
-__device__ __forceinline__ f32x4 reduce_col64(const float* ws, int nparts, int E, int e, f32x4 (*red)[16]) {
-  const int el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+// Wide form (rows whose length and base keep float4 alignment): block = 256 elements (64 lanes x 4) of every
+// partial row, each wave reading 1 KB of one row per load (4 rows at a time over the 4 waves, 8 rows in flight
+// per wave); the 8 per-thread sums, then the 4 waves, are combined in a fixed order: deterministic.
+constexpr int kRedCols256 = 256;
+__device__ __forceinline__ f32x4 reduce_col256(const float* ws, int nparts, int E, int e, f32x4 (*red)[64]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4 s[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (e < E) {
-    int p = grp;
-    for (; p + 7 * 16 < nparts; p += 8 * 16)
+    int p = wave;
+    for (; p + 4 * 7 < nparts; p += 4 * 8)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s[u] += *(const f32x4*)(ws + (size_t)(p + 16 * u) * E + e);
-    for (; p < nparts; p += 16) s[0] += *(const f32x4*)(ws + (size_t)p * E + e);
+      for (int u = 0; u < 8; ++u) s[u] += *(const f32x4*)(ws + (size_t)(p + 4 * u) * E + e);
+    for (; p < nparts; p += 4) s[0] += *(const f32x4*)(ws + (size_t)p * E + e);
   }
-  red[grp][el] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  red[wave][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   f32x4 t = {0.f, 0.f, 0.f, 0.f};
-  if (grp == 0)
-    for (int g = 0; g < 16; ++g) t += red[g][el];
+  if (wave == 0) t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
   return t;
 }
 
@@ -1292,9 +1292,9 @@ __global__ __launch_bounds__(256) void reduce_partials_batched_kernel(ReduceBatc
   while (i + 1 < rb.count && (int)blockIdx.x >= rb.start[i + 1]) ++i;
   const vqa_partials_desc& d = rb.d[i];
   if (rb.vec4[i]) {
-    const int e = ((int)blockIdx.x - rb.start[i]) * kRedCols4 + 4 * (threadIdx.x & 15);
-    const f32x4 s = reduce_col64(d.partials, d.nparts, d.n, e, red4);
-    if (threadIdx.x < 16 && e < d.n) {
+    const int e = ((int)blockIdx.x - rb.start[i]) * kRedCols256 + 4 * (threadIdx.x & 63);
+    const f32x4 s = reduce_col256(d.partials, d.nparts, d.n, e, (f32x4(*)[64])red4);
+    if (threadIdx.x < 64 && e < d.n) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int eq = e + q;
@@ -2087,7 +2087,7 @@ extern "C" int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vq
       rb.d[i] = d;
       rb.start[i] = blocks;
       rb.vec4[i] = desc_vec4(d) ? 1 : 0;
-      blocks += rb.vec4[i] ? (d.n + kRedCols4 - 1) / kRedCols4 : (d.n + kRedCols - 1) / kRedCols;
+      blocks += rb.vec4[i] ? (d.n + kRedCols256 - 1) / kRedCols256 : (d.n + kRedCols - 1) / kRedCols;
     }
     rb.start[rb.count] = blocks;
     hipLaunchKernelGGL(reduce_partials_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);

@@ -143,7 +143,7 @@ __device__ __forceinline__ float vq_unpack_dist(unsigned long long p) {
 // idx as packed keys through atomicMin (vq_argmin_unpack_kernel turns them into indices / distances).
 // Code chunks are double-buffered in LDS: the next chunk's global loads are in flight (registers) while the
 // current chunk runs its MFMAs, and land in the other buffer behind ONE barrier per chunk. Codes past the span
-// carry |e|^2 = +inf (their distance never wins), so the epilogue is add, fma, compare and two selects.
+// carry |e|^2 = +inf (their key is -inf and never wins), so the epilogue is one compare and two selects.
 template <int D>
 __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, const bf16* E3, const float* esq,
                                                              int64_t* idx, float* mind, long long N, int K,
@@ -188,14 +188,17 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
     for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(s, 4 * (lane >> 4) + r, 64);
   }
 
+  // the kernel maximises key = z.e - |e|^2 / 2 (distance = |z|^2 - 2 key): the MFMA accumulator starts at
+  // -|e|^2 / 2, so a code costs one compare and two selects per row (the distance form took an add and an fma
+  // more); the argmin is the distance's on every row whose top-2 margin exceeds the last-bit roundings
   float best[RT][4];
   int bidx[RT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      best[rt][r] = __builtin_inff();
-      bidx[rt][r] = kbeg;  // no finite distance in this span: (inf, first code); the merge keeps code 0
+      best[rt][r] = -__builtin_inff();
+      bidx[rt][r] = kbeg;  // no finite key in this span: (inf distance, first code); the merge keeps code 0
     }
 
   // chunk staging: piece e = threadIdx.x + 256 p of code e / PPC
@@ -234,10 +237,10 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) bfr[s][ks] = *(const bf16x8*)(eb + s * D + ks * 32);
       const int kg = k0 + kl;
-      const float e2 = el2[b][kl];
+      const float c = -0.5f * el2[b][kl];  // exact; codes past the span: -inf, never chosen
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        f32x4 acc = {c, c, c, c};
 #pragma unroll
         for (int s = 2; s >= 0; --s)  // smallest plane first
 #pragma unroll
@@ -245,10 +248,8 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt][ks], bfr[s][ks], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // (|z|^2 + |e|^2) - 2 z.e as TF evaluates it: 2 z.e is exact, so the fma rounds once like the sub
-          const float dist = __builtin_fmaf(-2.0f, acc[r], zq[rt][r] + e2);
-          if (dist < best[rt][r]) {
-            best[rt][r] = dist;
+          if (acc[r] > best[rt][r]) {  // strict: the lowest code wins a tie (codes visited in increasing order)
+            best[rt][r] = acc[r];
             bidx[rt][r] = kg;
           }
         }
@@ -267,18 +268,24 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
       for (int m = 1; m < 16; m <<= 1) {
         const float ob = __shfl_xor(b, m, 64);
         const int oi = __shfl_xor(bi, m, 64);
-        if (ob < b || (ob == b && oi < bi)) {
+        if (ob > b || (ob == b && oi < bi)) {
           b = ob;
           bi = oi;
         }
       }
       const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
       if ((lane & 15) == 0 && row < N) {
+        // |z|^2 - 2 key (+inf for a row with no finite key). A row with a non-finite |z|^2 has no finite distance
+        // to any code (inf - inf or NaN): code 0 of the span, as the distance form resolves it
+        const float zr = zq[rt][r];
+        const bool finite = zr < __builtin_inff();
+        const float dist = finite ? __builtin_fmaf(-2.0f, b, zr) : zr;
+        if (!finite) bi = kbeg;
         if (packed) {
-          atomicMin((unsigned long long*)idx + row, vq_pack(b, bi));
+          atomicMin((unsigned long long*)idx + row, vq_pack(dist, bi));
         } else {
           idx[row] = bi;
-          if (mind) mind[row] = b;
+          if (mind) mind[row] = dist;
         }
       }
     }
