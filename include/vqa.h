@@ -197,6 +197,12 @@ int vqa_vq_reset_rows(const void* z, float* RT, int64_t N_local, int64_t row_off
 int vqa_vq_ema_apply(float* E, float* ET, float* m_t, float* N_t, const float* m_sumT, const float* n_sum,
                      const float* RT, float gamma, float one_minus_gamma, float thresh, float* metrics,
                      int64_t* counter, int D, int K, vqa_stream_t stream);
+/* vqa_vq_ema_apply that also writes the codebook's derived state the next argmin reads, in the same pass:
+ * e_sqnorm (K) = |e_k|^2 (vqa_vq_sqnorm's bits) and E3 (K, 3, D) bf16 = the hi/mid/lo planes
+ * (vqa_vq_split_bf16x3's bits); either may be NULL. Replaces the :144-145 update plus the two follow-up launches. */
+int vqa_vq_ema_apply_derived(float* E, float* ET, float* m_t, float* N_t, const float* m_sumT, const float* n_sum,
+                             const float* RT, float gamma, float one_minus_gamma, float thresh, float* metrics,
+                             int64_t* counter, float* e_sqnorm, void* E3, int D, int K, vqa_stream_t stream);
 /* The reset permutation (host-callable; the device uses the same code): a keyed 4-round Feistel
  * bijection on [0, M) with cycle walking. Returns the k-th sampled row of the tiled batch. */
 int64_t vqa_reset_perm_index(uint64_t seed, int64_t counter, int level, int64_t M, int64_t k);

@@ -194,6 +194,42 @@ def test_ema_apply_matches_reference_formula(cuda):
     assert abs(float(met[2]) + float((p * torch.log(p + 1e-8)).sum())) < 1e-4
 
 
+@pytest.mark.parametrize("D,K", [(64, 2048), (8, 1024), (32, 70)])
+def test_ema_apply_derived_state_bitwise(cuda, D, K):
+    """vqa_vq_ema_apply_derived writes, in the EMA launch itself, the new codebook's |e|^2 and bf16 hi/mid/lo planes:
+    bitwise what vqa_vq_sqnorm and vqa_vq_split_bf16x3 give for the updated E (the next argmin's inputs), and the
+    EMA outputs bitwise those of vqa_vq_ema_apply."""
+    g = torch.Generator().manual_seed(D + K)
+    E = (torch.rand(D, K, generator=g) - 0.5) * 0.1
+    n_sum = torch.zeros(K)
+    n_sum[: K // 3] = torch.randint(1, 50, (K // 3,), generator=g).float()
+    m_sumT = torch.randn(K, D, generator=g) * n_sum[:, None]
+    RT = torch.randn(K, D, generator=g)
+    gam, omg = float(np.float32(0.99)), float(np.float32(1 - 0.99))
+    outs = []
+    for derived in (False, True):
+        Ed, ETd, mtd, Ntd = E.cuda(), E.t().contiguous().cuda(), E.clone().cuda(), torch.ones(K, device=cuda)
+        ctr = torch.zeros(1, dtype=torch.int64, device=cuda)
+        esq = torch.full((K,), float("nan"), device=cuda)
+        E3 = torch.zeros(K, 3, D, dtype=torch.bfloat16, device=cuda)
+        if derived:
+            V.vq_ema_apply(Ed, ETd, mtd, Ntd, m_sumT.cuda(), n_sum.cuda(), RT.cuda(), gam, omg, 1.0, None, ctr,
+                           esq=esq, E3=E3)
+        else:
+            V.vq_ema_apply(Ed, ETd, mtd, Ntd, m_sumT.cuda(), n_sum.cuda(), RT.cuda(), gam, omg, 1.0, None, ctr)
+            V.vq_sqnorm(Ed, esq)
+            V.vq_split_bf16x3(Ed, E3)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (Ed, ETd, mtd, Ntd, esq, E3)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    P = outs[1][5].float()
+    assert torch.equal((P[:, 0] + P[:, 1] + P[:, 2]).t(), outs[1][0])
+    # |e|^2 as the sum of squares of the fp32 codebook, to fp32 rounding of a 64-term sum
+    ref = (outs[1][0].double() ** 2).sum(0)
+    assert torch.allclose(outs[1][4].double(), ref, rtol=1e-6, atol=0)
+
+
 def test_vector_quantizer_layer_call(cuda):
     """VectorQuantizer.py:204-221 smoke: K=6, D=2 — the generic (D not MFMA-tiled) path."""
     torch.manual_seed(0)

@@ -164,9 +164,10 @@ class VectorQuantizer:
         return dz.view(dq.shape)
 
     def apply_ema(self, update_trackers: bool = True):
+        # the new codebook's |e|^2 and bf16 planes (the next argmin's inputs) come out of the same launch
         V.vq_ema_apply(self.embeddings, self.ET, self.m_t, self.N_t, self.m_sumT, self.n_sum, self.RT, self._g,
-                       self._omg, float(self.codebook_usage_threshold), self.vq_metrics, self.calls)
-        self._codebook_changed()
+                       self._omg, float(self.codebook_usage_threshold), self.vq_metrics, self.calls,
+                       esq=self.e_sqnorm, E3=self.E3)
         if update_trackers:
             self.batch_usage_tracker.update_state(self.vq_metrics[0])
             self.usage_tracker.update_state(self.vq_metrics[1])

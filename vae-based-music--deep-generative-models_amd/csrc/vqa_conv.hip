@@ -1292,9 +1292,33 @@ __global__ __launch_bounds__(256) void reduce_partials_batched_kernel(ReduceBatc
   while (i + 1 < rb.count && (int)blockIdx.x >= rb.start[i + 1]) ++i;
   const vqa_partials_desc& d = rb.d[i];
   if (rb.vec4[i]) {
+#ifdef VQA_REDUCE_COL64  // A/B only: the round-3 layout (64 columns x 16 row groups per block)
+    const int e = ((int)blockIdx.x - rb.start[i]) * 64 + 4 * (threadIdx.x & 15);
+    f32x4 s;
+    {
+      const int el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e < d.n) {
+        int p = grp;
+        for (; p + 7 * 16 < d.nparts; p += 8 * 16)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) t[u] += *(const f32x4*)(d.partials + (size_t)(p + 16 * u) * d.n + e);
+        for (; p < d.nparts; p += 16) t[0] += *(const f32x4*)(d.partials + (size_t)p * d.n + e);
+      }
+      red4[grp][el] = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+      __syncthreads();
+      s = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (grp == 0)
+        for (int g = 0; g < 16; ++g) s += red4[g][el];
+    }
+    if (threadIdx.x < 16 && e < d.n) {
+#else
     const int e = ((int)blockIdx.x - rb.start[i]) * kRedCols256 + 4 * (threadIdx.x & 63);
     const f32x4 s = reduce_col256(d.partials, d.nparts, d.n, e, (f32x4(*)[64])red4);
     if (threadIdx.x < 64 && e < d.n) {
+#endif
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int eq = e + q;
@@ -2087,7 +2111,11 @@ extern "C" int vqa_reduce_partials(const vqa_partials_desc* descs, int count, vq
       rb.d[i] = d;
       rb.start[i] = blocks;
       rb.vec4[i] = desc_vec4(d) ? 1 : 0;
+#ifdef VQA_REDUCE_COL64
+      blocks += rb.vec4[i] ? (d.n + 63) / 64 : (d.n + kRedCols - 1) / kRedCols;
+#else
       blocks += rb.vec4[i] ? (d.n + kRedCols256 - 1) / kRedCols256 : (d.n + kRedCols - 1) / kRedCols;
+#endif
     }
     rb.start[rb.count] = blocks;
     hipLaunchKernelGGL(reduce_partials_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);

@@ -237,6 +237,27 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) bfr[s][ks] = *(const bf16x8*)(eb + s * D + ks * 32);
       const int kg = k0 + kl;
+#ifdef VQA_ARGMIN_DIST_FORM  // A/B only: the round-3 distance-form epilogue (add, fma, compare, two selects)
+      const float e2 = el2[b][kl];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 2; s >= 0; --s)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt][ks], bfr[s][ks], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // timing only (best holds -distance; the reported min distance is not meaningful in this build)
+          const float dist = __builtin_fmaf(-2.0f, acc[r], zq[rt][r] + e2);
+          if (-dist > best[rt][r]) {
+            best[rt][r] = -dist;
+            bidx[rt][r] = kg;
+          }
+        }
+      }
+#else
       const float c = -0.5f * el2[b][kl];  // exact; codes past the span: -inf, never chosen
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
@@ -254,6 +275,7 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
           }
         }
       }
+#endif
     }
     if (more) store_chunk(b ^ 1);  // buffer b ^ 1 was last read before the previous barrier
     __syncthreads();
@@ -346,15 +368,18 @@ __global__ __launch_bounds__(256) void vq_argmin_direct_kernel(const T* z, const
   if (mind) mind[n] = best;
 }
 
+// |e_k|^2, one wave per code: lane d squares e[d][k] (d, d + 64, ... for D > 64), then a butterfly sum over the
+// wave — the summation order of vq_ema_apply_kernel's fused |e|^2, so both give the same bits for the same E
 __global__ __launch_bounds__(256) void vq_sqnorm_kernel(const float* E, float* esq, int D, int K) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (k >= K) return;  // wave-uniform
   float s = 0.f;
-  for (int d = 0; d < D; ++d) {
+  for (int d = lane; d < D; d += 64) {
     const float v = E[(long long)d * K + k];
     s += v * v;
   }
-  esq[k] = s;
+  s = warp_sum(s);
+  if (lane == 0) esq[k] = s;
 }
 
 // ---- quantize / straight-through / commitment ----------------------------------------------------
@@ -418,24 +443,44 @@ __global__ __launch_bounds__(256) void vq_reset_rows_kernel(const T* z, float* R
 }
 
 // one wave per code, lane = d (D <= 64)
+// One wave per code k, lane d = embedding dimension. With esq / E3 (nullable) the codebook's derived state is
+// written in the same pass: |e_k|^2 (the butterfly order of vq_sqnorm_kernel) and the bf16 hi/mid/lo planes
+// (vq_split3_kernel's arithmetic) — the two launches the next step's argmin needs, off the step's serial tail.
 __global__ __launch_bounds__(256) void vq_ema_apply_kernel(float* E, float* ET, float* m_t, float* N_t,
                                                           const float* m_sumT, const float* n_sum, const float* RT,
-                                                          float g, float omg, float thresh, int64_t* counter, int D,
-                                                          int K) {
+                                                          float g, float omg, float thresh, int64_t* counter,
+                                                          float* esq, bf16* E3, int D, int K) {
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int d = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;
-  if (k >= K || d >= D) return;
-  // TF: gamma * N_t + (1 - gamma) * N_t_  — two products then a sum (no contraction: -ffp-contract=off)
-  const float Nn = g * N_t[k] + omg * n_sum[k];
-  const float mn = g * m_t[(long long)d * K + k] + omg * m_sumT[(long long)k * D + d];
-  const bool use = Nn >= thresh;
-  const float Nc = fminf(fmaxf(Nn, 1e-8f), 1e8f);
-  const float e = use ? mn / Nc : RT[(long long)k * D + d];
-  m_t[(long long)d * K + k] = mn;
-  E[(long long)d * K + k] = e;
-  ET[(long long)k * D + d] = e;
-  if (d == 0) N_t[k] = Nn;
+  if (k >= K) return;  // wave-uniform
+  float e = 0.f;
+  if (d < D) {
+    // TF: gamma * N_t + (1 - gamma) * N_t_  — two products then a sum (no contraction: -ffp-contract=off)
+    const float Nn = g * N_t[k] + omg * n_sum[k];
+    const float mn = g * m_t[(long long)d * K + k] + omg * m_sumT[(long long)k * D + d];
+    const bool use = Nn >= thresh;
+    const float Nc = fminf(fmaxf(Nn, 1e-8f), 1e8f);
+    e = use ? mn / Nc : RT[(long long)k * D + d];
+    m_t[(long long)d * K + k] = mn;
+    E[(long long)d * K + k] = e;
+    ET[(long long)k * D + d] = e;
+    if (d == 0) N_t[k] = Nn;
+    if (E3) {
+      const bf16 hi = (bf16)e;
+      const float r1 = e - (float)hi;
+      const bf16 mid = (bf16)r1;
+      const bf16 lo = (bf16)(r1 - (float)mid);
+      bf16* o = E3 + (size_t)k * 3 * D + d;
+      o[0] = hi;
+      o[D] = mid;
+      o[2 * D] = lo;
+    }
+  }
+  if (esq) {
+    const float s = warp_sum(e * e);
+    if (d == 0) esq[k] = s;
+  }
 }
 
 // metrics: [0] #(n_sum >= thr), [1] #(N_t >= thr), [2] -sum p log(p + 1e-8), p = n_sum / sum(n_sum)
@@ -709,7 +754,7 @@ using namespace vqa;
 
 extern "C" int vqa_vq_sqnorm(const float* E, float* e_sqnorm, int D, int K, vqa_stream_t stream) {
   VQA_ARG(E && e_sqnorm && D > 0 && K > 0, "vq_sqnorm: bad arguments");
-  hipLaunchKernelGGL(vq_sqnorm_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, E, e_sqnorm, D, K);
+  hipLaunchKernelGGL(vq_sqnorm_kernel, dim3((K + 3) / 4), dim3(256), 0, (hipStream_t)stream, E, e_sqnorm, D, K);
   VQA_LAUNCHED("vq_sqnorm_kernel");
   return VQA_OK;
 }
@@ -861,11 +906,19 @@ extern "C" int vqa_vq_reset_rows(const void* z, float* RT, int64_t N_local, int6
 extern "C" int vqa_vq_ema_apply(float* E, float* ET, float* m_t, float* N_t, const float* m_sumT, const float* n_sum,
                                 const float* RT, float gamma, float one_minus_gamma, float thresh, float* metrics,
                                 int64_t* counter, int D, int K, vqa_stream_t stream) {
+  return vqa_vq_ema_apply_derived(E, ET, m_t, N_t, m_sumT, n_sum, RT, gamma, one_minus_gamma, thresh, metrics, counter,
+                                  nullptr, nullptr, D, K, stream);
+}
+
+extern "C" int vqa_vq_ema_apply_derived(float* E, float* ET, float* m_t, float* N_t, const float* m_sumT,
+                                        const float* n_sum, const float* RT, float gamma, float one_minus_gamma,
+                                        float thresh, float* metrics, int64_t* counter, float* e_sqnorm, void* E3,
+                                        int D, int K, vqa_stream_t stream) {
   VQA_ARG(E && ET && m_t && N_t && m_sumT && n_sum && RT && counter, "vq_ema_apply: null pointer");
   VQA_ARG(D > 0 && D <= 64 && K > 0, "vq_ema_apply: supports D <= 64 (got D=%d)", D);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(vq_ema_apply_kernel, dim3((K + 3) / 4), dim3(256), 0, s, E, ET, m_t, N_t, m_sumT, n_sum, RT, gamma,
-                     one_minus_gamma, thresh, counter, D, K);
+                     one_minus_gamma, thresh, counter, e_sqnorm, (bf16*)E3, D, K);
   VQA_LAUNCHED("vq_ema_apply_kernel");
   if (metrics) {
     hipLaunchKernelGGL(vq_metrics_kernel, dim3(1), dim3(256), 0, s, n_sum, (const float*)N_t, thresh, K, metrics);

@@ -26,7 +26,7 @@ EXPORTED = [
     "vqa_conv1d_transpose_fwd", "vqa_conv1d_transpose_bwd_data", "vqa_conv1d_transpose_bwd_weight",
     "vqa_conv1d_transpose_bwd_weight_workspace",
     "vqa_vq_sqnorm", "vqa_vq_argmin", "vqa_vq_quantize", "vqa_vq_quantize_workspace", "vqa_vq_backward",
-    "vqa_vq_reset_rows", "vqa_vq_ema_apply", "vqa_reset_perm_index",
+    "vqa_vq_reset_rows", "vqa_vq_ema_apply", "vqa_vq_ema_apply_derived", "vqa_reset_perm_index",
     "vqa_mse_loss", "vqa_mse_loss_workspace", "vqa_adam_keras", "vqa_lr_schedule", "vqa_counter_add",
     "vqa_conv1d_bwd_weight_partials", "vqa_conv1d_transpose_bwd_weight_partials", "vqa_reduce_partials",
     "vqa_conv1d_bwd_data_weight", "vqa_conv1d_bwd_data_weight_workspace",
@@ -81,6 +81,7 @@ _SIGS = {
     "vqa_vq_backward": (_I, [_P, _P, _P, _P, _P, _F, _L, _I, _I, _P]),
     "vqa_vq_reset_rows": (_I, [_P, _P, _L, _L, _L, _I, _I, _U, _P, _I, _I, _P]),
     "vqa_vq_ema_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P, _I, _I, _P]),
+    "vqa_vq_ema_apply_derived": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P, _I, _I, _P]),
     "vqa_reset_perm_index": (_L, [_U, _L, _I, _L, _L]),
     "vqa_mse_loss": (_I, [_P, _P, _P, _P, _P, _L, _P, _S, _P]),
     "vqa_mse_loss_workspace": (_S, [_L]),
@@ -408,10 +409,14 @@ def vq_reset_rows(z, RT, row_offset, N_global, seed, counter, level):
                                    dtype_code(z.dtype), stream()), "vqa_vq_reset_rows")
 
 
-def vq_ema_apply(E, ET, m_t, N_t, m_sumT, n_sum, RT, gamma, omg, thresh, metrics, counter):
+def vq_ema_apply(E, ET, m_t, N_t, m_sumT, n_sum, RT, gamma, omg, thresh, metrics, counter, esq=None, E3=None):
+    """EMA + dead-code reset; with esq / E3 also |e|^2 and the bf16 planes of the new codebook (same pass)."""
     D, K = E.shape
-    _check(lib().vqa_vq_ema_apply(ptr(E), ptr(ET), ptr(m_t), ptr(N_t), ptr(m_sumT), ptr(n_sum), ptr(RT), gamma, omg,
-                                  thresh, ptr(metrics), ptr(counter), D, K, stream()), "vqa_vq_ema_apply")
+    if E3 is not None and (E3.dtype != torch.bfloat16 or tuple(E3.shape) != (K, 3, D)):
+        raise VQAError(f"vq_ema_apply: E3 must be ({K}, 3, {D}) bf16")
+    _check(lib().vqa_vq_ema_apply_derived(ptr(E), ptr(ET), ptr(m_t), ptr(N_t), ptr(m_sumT), ptr(n_sum), ptr(RT), gamma,
+                                          omg, thresh, ptr(metrics), ptr(counter), ptr(esq), ptr(E3), D, K, stream()),
+           "vqa_vq_ema_apply_derived")
 
 
 def mse_loss(x, r, extra, dr, loss_out):
