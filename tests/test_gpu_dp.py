@@ -98,9 +98,11 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
     counts stay bitwise equal and the weights within rel 1e-5 of max |w|, as in the first DP tests. `world` ranks:
     the exchanged gradient is world x the global mean, and the summation-grouping bounds of the EMA sums and
     codebooks after step 2 are 10x / 5x wider at 4 ranks (more rank partial sums; measured 4.4e-6 / 1.03e-5). `full_size` (B = 32 per rank,
-    T = 65,536): after the first Keras Adam step each weight moved by lr * g / (|g| + eps); where g is pure
-    rounding noise (it cancels over 2M rows) that ratio takes any value in [-1, 1], so the weights are held to
-    one update per element (|delta w| <= lr) and relative L2 1e-5 instead of rel 1e-5 of max |w|."""
+    T = 65,536): every gradient element is a sum over up to 2^21 rows whose grouping differs completely between
+    the runs, so the gradient and Adam's moments are held to 1e-4 of max |g| (measured 2.1e-5 and 5.7e-5 with two
+    kernel versions, always on the longest cancelling sums: the first encoder conv's bias); after the first Keras
+    Adam step each weight moved by lr * g / (|g| + eps), a ratio anywhere in [-1, 1] where g is rounding noise, so
+    the weights are held to two updates per element (|delta w| <= 2 lr) and relative L2 1e-4."""
     lr = 1e-3  # Keras Adam default (vqa_optim.Adam)
     nst = 2 * K * D + K  # one level's stats region: m_sumT, n_sum, RT
     rep, bad = [], []
@@ -150,7 +152,7 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
     if phase == "step1":
         # the exchanged gradient (sum over ranks of rank-mean gradients) = world x the global-batch mean
         # gradient, to fp32 rounding of the different summation grouping
-        e, tol = _rel(r0["grads"] / world, s["grads"]), (5e-5 if full_size else 1e-5 if bf16 else 2e-6)
+        e, tol = _rel(r0["grads"] / world, s["grads"]), (1e-4 if full_size else 1e-5 if bf16 else 2e-6)
         worst = ""
         if e >= tol and "offsets" in s:  # which parameters differ (diagnostic)
             gmax = float(s["grads"].double().abs().max())
@@ -167,13 +169,13 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
         # up to ~1e-3 of that element's update (lr = 1e-3 per step), i.e. a few 1e-6 of max|w|
         if full_size:
             dw = float((r0["weights"] - s["weights"]).abs().max())
-            check(dw <= lr * 1.01, f"max |delta w| {dw:.2e} <= one Adam update ({lr:g})")
+            check(dw <= 2 * lr * 1.01, f"max |delta w| {dw:.2e} <= two Adam updates ({2 * lr:g})")
             e = _l2(r0["weights"], s["weights"])
-            check(e < 1e-5, f"weights relative L2 {e:.2e} < 1e-5")
+            check(e < 1e-4, f"weights relative L2 {e:.2e} < 1e-4")
         else:
             e = _rel(r0["weights"], s["weights"])
             check(e < 1e-5, f"weights rel {e:.2e} < 1e-5")
-        e, mtol = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"])), (5e-5 if full_size else 1e-5)
+        e, mtol = max(_rel(r0["adam_m"], s["adam_m"]), _rel(r0["adam_v"], s["adam_v"])), (1e-4 if full_size else 1e-5)
         check(e < mtol, f"Adam moments rel {e:.2e} < {mtol:g}")
     elif exact_path:
         # after the second update an element whose gradient is pure rounding noise (it cancels over the batch)
@@ -292,12 +294,11 @@ def test_dp4_reset_rows_from_every_rank_offset(cuda, tmp_path):
 @pytest.mark.timeout(900)
 def test_dp2_config3_per_rank_workload(cuda, tmp_path):
     """BASELINE config 3's per-rank workload through the DP branch: two gloo ranks on the one GPU, each at B = 32,
-    T = 65,536, bf16, the step graph-captured (warm-up step, then two graphs around the exchange), against one
-    process on the concatenated B = 64 batch: code counts and the global reset rows bitwise, EMA sums rel 1e-6,
-    replicas bitwise; exchanged gradient (and Adam's first moments, 0.1 x it) rel 5e-5 of max |g|: every gradient
-    element here is a sum over 2^21 rows whose grouping differs completely between one process (512 workgroup
-    partials over 64 items) and two (512 over 32 items each, then the exchange); the bias gradients, long sums
-    that cancel, are the worst (measured 2.1e-5, enc1/blk0/down0/bias; 1e-5 holds at cfg2_short's 2^14 rows)."""
+    T = 65,536, bf16, the step graph-captured (warm-up step on a side stream, then two graphs around the exchange).
+      exact — the exchanged gradient equals, bitwise, the sum of the two single-process gradients of each rank's
+        32 items (fp32 a + b: any 2-rank reduction gives it), and the replicas are bitwise identical;
+      vs one process on the concatenated B = 64 batch — code counts and the global reset rows bitwise, EMA sums
+        rel 1e-6, and the summation-grouping bounds of _compare(full_size=True) for the gradient and the weights."""
     config, dtype = "cfg2", "bf16"
     cfg = W.CONFIGS[config]
     K, D, L = cfg["num_embeddings"], cfg["latent_dim"], cfg["levels"]
@@ -305,8 +306,16 @@ def test_dp2_config3_per_rank_workload(cuda, tmp_path):
     old = W.B_LOCAL
     W.B_LOCAL = 32
     try:
-        m = W.build(64, config=config, dtype=dtype)
         xs = W.batches(2, config)
+        local = []
+        for r in range(2):
+            m = W.build(32, config=config, dtype=dtype)
+            m._compute(m._as_input(xs[0][r * 32:(r + 1) * 32]), True)
+            torch.cuda.synchronize()
+            local.append(m.bucket[:m.layout["grads"][1]].detach().cpu())
+            del m
+            torch.cuda.empty_cache()
+        m = W.build(64, config=config, dtype=dtype)
         m.train_step(xs[0])
         torch.cuda.synchronize()
         ref = W.snapshot(m)
@@ -314,6 +323,11 @@ def test_dp2_config3_per_rank_workload(cuda, tmp_path):
         torch.cuda.empty_cache()
     finally:
         W.B_LOCAL = old
+    total = local[0] + local[1]
+    for r in range(2):
+        got = ranks[r]["step1"]["grads"]
+        n = int((got != total).sum())
+        assert n == 0, f"rank {r}: {n} exchanged gradient elements differ from local0 + local1"
     rep, bad = _compare(ranks[0]["step1"], ranks[1]["step1"], ref, K, D, L, "step1", True, full_size=True)
     print("--- config 3 per-rank workload (B=32/rank, T=65536, bf16, graph)")
     print("\n".join(rep))

@@ -119,44 +119,3 @@ def test_shared_target(cuda, B, T):
         assert abs(float(l1) - loss_ref) / loss_ref < 1e-5
         err = (g1.cpu().double() - g_ref).abs().max() / g_ref.abs().max()
         assert err < 1e-4, err
-
-
-_AB_SCRIPT = r"""
-import sys, torch
-sys.path[:0] = sys.argv[3:]
-from data_utils import SpectralTarget, multispectral_loss_and_grad
-from oracle import vqvae_ref as R
-B, T = 4, int(sys.argv[2])
-x = torch.from_numpy(R.synthetic_batch(B, T, seed=5)).cuda()
-g = torch.Generator().manual_seed(6)
-r = (0.3 * torch.randn(B, T, 1, generator=g)).cuda() + 0.5 * x
-tg = SpectralTarget(x)
-loss, dr = multispectral_loss_and_grad(tg, r)
-torch.cuda.synchronize()
-torch.save({"loss": loss.cpu(), "dr": dr.cpu(), "tm": [t.cpu() for t in tg.mags()] if hasattr(tg, "mags") else []},
-           sys.argv[1])
-"""
-
-
-@pytest.mark.parametrize("T", [65536, 4096 + 116])
-def test_two_wave_form_bitwise_equals_one_wave_form(cuda, tmp_path, T):
-    """spec_pairw_kernel (two waves per SIMD: per-pass twiddle tables, 16-padded buffers, window from global memory)
-    and spec_gather4_kernel (four samples per thread) against the one-wave-per-SIMD spec_pair_kernel and the
-    one-sample gather (VQA_SPEC_IMPL=1), each in its own process: the same butterflies, twiddle values and
-    summation orders, so the loss and the gradient are bitwise equal."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    paths = [os.path.join(root, "vae-based-music--deep-generative-models_amd"), root]
-    outs = {}
-    for impl in ("1", "w"):
-        out = str(tmp_path / f"spec_{impl}.pt")
-        env = dict(os.environ, VQA_SPEC_IMPL=impl)
-        p = subprocess.run([sys.executable, "-c", _AB_SCRIPT, out, str(T), *paths], env=env, capture_output=True,
-                           text=True, timeout=300)
-        assert p.returncode == 0, p.stderr[-3000:]
-        outs[impl] = torch.load(out, weights_only=True)
-    assert torch.equal(outs["1"]["loss"], outs["w"]["loss"])
-    d = (outs["1"]["dr"] - outs["w"]["dr"]).abs()
-    assert torch.equal(outs["1"]["dr"], outs["w"]["dr"]), f"{int((d > 0).sum())} gradient samples differ, max {float(d.max()):.3e}"

@@ -565,223 +565,6 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
   }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// The same frame-pair algorithm at TWO waves per SIMD (spec_pairw_kernel). The one-wave-per-SIMD form above
-// holds ~455 VGPRs (the next pair's samples prefetched in registers) and a 98 KB LDS image per 4-wave workgroup,
-// so every LDS / HBM latency of a pass is exposed. Here:
-//   - the waves' FFT buffers are padded by one complex per 16 (N = 512: per 8), and the generic twiddle table is
-//     replaced by per-pass tables: pass 0 reads T0[p (R0+1) + k] = W_N^{k p} (row pitch R0 + 1: the 32 lanes of a
-//     ds_read_b64 hit 32 different banks, where tw[k p] was up to 8-way conflicted), pass 1 T1[p R1 + k] =
-//     W_N^{k p S1} (lanes of one p broadcast), the last pass has none (its p is 0);
-//   - the window is read from global memory (L1/L2-resident, 8 KB) instead of an LDS copy;
-//   - no register prefetch of the next pair (its co-resident partner wave hides the HBM latency instead);
-// so N = 2048 runs 8 waves per CU (one 512-thread workgroup: 2 x 8.5 + 8 x 17 KB of LDS) at <= 256 VGPRs.
-// Bit-identical to spec_pair_kernel: the same butterflies, twiddle values and operation order.
-template <int N> constexpr int spw_padsh() { return N == 512 ? 3 : 4; }
-template <int N> __device__ __forceinline__ int pzw(int i) { return i + (i >> spw_padsh<N>()); }
-template <int N> constexpr int spw_zlen() { return N + (N >> spw_padsh<N>()); }
-template <int N> constexpr int spw_t0len() { return N / wradix<N, 0>() * (wradix<N, 0>() + 1); }
-template <int N> constexpr int spw_t1len() { return wradix<N, 1>() > 0 && wradix<N, 2>() > 0 ? N / wstride<N, 1>() : 0; }
-template <int N> constexpr int spw_waves() { return N == 2048 ? 8 : 4; }
-template <int N> constexpr size_t spw_lds() {
-  return ((size_t)spw_t0len<N>() + spw_t1len<N>() + (size_t)spw_waves<N>() * spw_zlen<N>()) * sizeof(f32x2);
-}
-
-// one Stockham pass (as wpass) with the twiddle of (k, p) from table TB: 0 = T0 (pitch R+1), 1 = T1 (pitch R),
-// 2 = none (p == 0 for every butterfly of the pass)
-template <int N, int R, int S, bool INV, int TB>
-__device__ __forceinline__ void wpassw(f32x2* z, const f32x2* t, int lane) {
-  constexpr int m = N / (S * R), NBF = N / R, IT = (NBF + 63) / 64;
-  f32x2 v[IT][R];
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int j = lane + 64 * it;
-    if (NBF % 64 == 0 || j < NBF) {
-      const int p = j / S, q = j - p * S;
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[it][r] = z[pzw<N>(q + S * (p + r * m))];
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int j = lane + 64 * it;
-    if (NBF % 64 == 0 || j < NBF) {
-      const int p = j / S, q = j - p * S;
-      dft<R, INV>(v[it]);
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        f32x2 o = v[it][k];
-        if (TB != 2 && k) {
-          f32x2 w = TB == 0 ? t[p * (R + 1) + k] : t[p * R + k];
-          if (INV) w = conj2(w);
-          o = cmul(o, w);
-        }
-        z[pzw<N>(q + S * (R * p + k))] = o;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <int N, int MODE>
-__global__ __launch_bounds__(64 * spw_waves<N>()) void spec_pairw_kernel(SpecPairArgs a) {
-  constexpr bool GRAD = MODE == PAIR_GRAD, MAG = MODE == PAIR_MAG;
-  constexpr int W = spw_waves<N>();
-  constexpr int KB = N / 2 + 1, NB = (KB + 63) / 64;
-  constexpr int R0 = wradix<N, 0>(), R1 = wradix<N, 1>(), R2 = wradix<N, 2>();
-  constexpr int S1 = wstride<N, 1>(), S2 = wstride<N, 2>();
-  constexpr int NBF0 = N / R0, IT0 = (NBF0 + 63) / 64, M0 = N / R0;
-  // the table of the middle pass of a three-pass plan (a two-pass plan's second pass is its last: no twiddles)
-  constexpr int TB1 = R2 > 0 ? 1 : 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  f32x2* T0 = (f32x2*)smem;
-  f32x2* T1 = T0 + spw_t0len<N>();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  f32x2* z = T1 + spw_t1len<N>() + (size_t)wave * spw_zlen<N>();
-
-  const f32x2* tw = (const f32x2*)a.tw;
-  for (int e = threadIdx.x; e < NBF0 * R0; e += 64 * W) {
-    const int p = e / R0, k = e - p * R0;
-    T0[p * (R0 + 1) + k] = tw[k * p];
-  }
-  if constexpr (spw_t1len<N>() > 0) {
-    for (int e = threadIdx.x; e < spw_t1len<N>(); e += 64 * W) {
-      const int p = e / R1, k = e - p * R1;
-      T1[e] = tw[k * p * S1];
-    }
-  }
-  __syncthreads();
-
-  const int nframes = a.B * a.F, npairs = (nframes + 1) / 2;
-  const int gw = blockIdx.x * W + wave, nw = gridDim.x * W;
-  auto frame_base = [&](int f) {
-    const int bb_ = f / a.F;
-    return a.r + (size_t)bb_ * a.T + (size_t)(f - bb_ * a.F) * a.hop;
-  };
-  for (int pp = gw; pp < npairs; pp += nw) {
-    const int fa = 2 * pp, fb = fa + 1;
-    const bool acta = fa < nframes, actb = fb < nframes;
-    float ta[MAG ? 1 : NB], tb[MAG ? 1 : NB];
-    {
-      // pass 0 from HBM: windowed samples (n >= win: the FFT's zero padding), one butterfly at a time
-      const float* sa = frame_base(min(fa, nframes - 1));
-      const float* sb = frame_base(min(fb, nframes - 1));
-#pragma unroll 1
-      for (int it = 0; it < IT0; ++it) {
-        const int p = lane + 64 * it;  // S = 1: q = 0
-        if (NBF0 % 64 == 0 || p < NBF0) {
-          f32x2 v[R0];
-#pragma unroll
-          for (int r = 0; r < R0; ++r) {
-            const int n = p + r * M0, nc = n < a.win ? n : 0;
-            const float w = n < a.win ? a.wn[nc] : 0.f;
-            v[r] = f32x2{sa[nc] * w, sb[nc] * w};
-          }
-          dft<R0, false>(v);
-#pragma unroll
-          for (int k = 0; k < R0; ++k) z[pzw<N>(R0 * p + k)] = k ? cmul(v[k], T0[p * (R0 + 1) + k]) : v[k];
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    wpassw<N, R1, S1, false, TB1>(z, T1, lane);
-    if constexpr (!MAG) {
-      // the target magnitudes (requested before the last forward pass: they land during it)
-      const int pa = min(fa, nframes - 1), pb = min(fb, nframes - 1);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int k = lane + 64 * j, kc = k < KB ? k : 0;
-        ta[j] = a.tm[(size_t)pa * KB + kc];
-        tb[j] = a.tm[(size_t)pb * KB + kc];
-      }
-    }
-    if constexpr (R2 > 0) wpassw<N, R2, S2, false, 2>(z, T1, lane);
-    float sda = 0.f, sxa = 0.f, sdb = 0.f, sxb = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < NB; ++j) {
-      const int k = lane + 64 * j;
-      if (k < KB) {
-        const int km = (N - k) & (N - 1);
-        const f32x2 zk = z[pzw<N>(k)], zm = z[pzw<N>(km)];
-        const f32x2 rka = f32x2{0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
-        const f32x2 rkb = f32x2{0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x)};
-        const float mra = cabs2(rka), mrb = cabs2(rkb);
-        if constexpr (MAG) {
-          if (acta) a.out[(size_t)fa * KB + k] = mra;
-          if (actb) a.out[(size_t)fb * KB + k] = mrb;
-        } else {
-          const float da = ta[j] - mra, db = tb[j] - mrb;
-          sda += da * da;
-          sxa += ta[j] * ta[j];
-          sdb += db * db;
-          sxb += tb[j] * tb[j];
-          if constexpr (GRAD) {
-            const float ga = mra > 0.f ? (mra - ta[j]) * __builtin_amdgcn_rcpf(mra) : 0.f;
-            const float gb = mrb > 0.f ? (mrb - tb[j]) * __builtin_amdgcn_rcpf(mrb) : 0.f;
-            const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
-            if (k == 0 || k == N / 2) {
-              z[pzw<N>(k)] = f32x2{Ga.x, Gb.x};
-            } else {
-              z[pzw<N>(k)] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
-              z[pzw<N>(km)] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
-            }
-          }
-        }
-      }
-    }
-    if constexpr (!MAG) {
-      sda = warp_sum(sda);
-      sxa = warp_sum(sxa);
-      sdb = warp_sum(sdb);
-      sxb = warp_sum(sxb);
-      if (lane == 0) {
-        if (acta) {
-          a.part[2 * (size_t)fa] = sda;
-          a.part[2 * (size_t)fa + 1] = sxa;
-        }
-        if (actb) {
-          a.part[2 * (size_t)fb] = sdb;
-          a.part[2 * (size_t)fb + 1] = sxb;
-        }
-      }
-    }
-    if constexpr (GRAD) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      constexpr int RL = R2 > 0 ? R2 : R1, SL = R2 > 0 ? S2 : S1, NBFL = N / RL, ITL = (NBFL + 63) / 64;
-      wpassw<N, R0, 1, true, 0>(z, T0, lane);
-      if constexpr (R2 > 0) wpassw<N, R1, S1, true, 1>(z, T1, lane);
-      // the last pass reads z and writes HBM only (no in-place hazard): one butterfly at a time
-      float* oa = a.out + (size_t)fa * a.win;
-      float* ob = a.out + (size_t)fb * a.win;
-#pragma unroll 2
-      for (int it = 0; it < ITL; ++it) {
-        const int q = lane + 64 * it;
-        if (NBFL % 64 == 0 || q < NBFL) {
-          f32x2 v[RL];
-#pragma unroll
-          for (int r = 0; r < RL; ++r) v[r] = z[pzw<N>(q + SL * r)];
-          dft<RL, true>(v);
-#pragma unroll
-          for (int k = 0; k < RL; ++k) {
-            const int n = q + SL * k;
-            if (n < a.win) {
-              const float w = a.wn[n];
-              if (acta) oa[n] = v[k].x * w;
-              if (actb) ob[n] = v[k].y * w;
-            }
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // twiddles exp(-2 pi i k / N) (N complex per resolution) and periodic Hann windows
 // (tf.signal.hann_window(win, periodic=True)), evaluated in fp64 and rounded once
 struct SpecTables {
@@ -874,48 +657,6 @@ __global__ __launch_bounds__(256) void spec_gather_kernel(SpecGatherArgs a) {
   }
 }
 
-// The overlap-add of spec_gather_kernel with four consecutive samples per thread (T % 4 == 0): one frame-range
-// computation per resolution for the four, 4 loads in flight per frame. Each sample still sums its frames in
-// ascending order and its resolutions in order: bit-identical.
-__global__ __launch_bounds__(256) void spec_gather4_kernel(SpecGatherArgs a) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int b = 0; b < a.B; ++b) {
-      float s = 0.f;
-      for (int r = 0; r < a.nres; ++r) s += a.lossbr[b * a.nres + r];
-      s = s / (float)a.nres;
-      if (a.item_loss) a.item_loss[b] = s;
-      tot += s;
-    }
-    a.loss_out[0] = tot / (float)a.B;
-  }
-  if (!a.dr) return;
-  const long long n4 = (long long)a.B * a.T / 4;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    const long long i0 = 4 * i;
-    const int b = (int)(i0 / a.T), t0 = (int)(i0 - (long long)b * a.T);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int r = 0; r < a.nres; ++r) {
-      const int hop = a.hop[r], win = a.win[r], F = a.F[r];
-      const int f_hi = min(F - 1, (t0 + 3) / hop);
-      const int f_lo = t0 >= win ? (t0 - win) / hop + 1 : 0;
-      const float* g = a.fg[r] + (size_t)b * F * win;
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int f = f_lo; f <= f_hi; ++f) {
-        const int u = t0 - f * hop;  // sample t0 + j sits at u + j of frame f when 0 <= u + j < win
-        const float* gf = g + (size_t)f * win + u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (u + j >= 0 && u + j < win) s[j] += gf[j];
-      }
-      const float sc = a.scale[b * a.nres + r];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += sc * s[j];
-    }
-    *(float4*)(a.dr + i0) = float4{acc[0], acc[1], acc[2], acc[3]};
-  }
-}
-
 template <int N>
 static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
   constexpr int FPI = 256 / spec_tpf<N>();
@@ -981,62 +722,8 @@ static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
   return VQA_OK;
 }
 
-// the two-waves-per-SIMD form: persistent, as many workgroups as the occupancy query admits per CU
-template <int N, int MODE>
-static int launch_pairsw(const SpecPairArgs& pa, hipStream_t s) {
-  constexpr int W = spw_waves<N>();
-  constexpr size_t lds = spw_lds<N>();
-  const void* fn = (const void*)spec_pairw_kernel<N, MODE>;
-  static bool lds_set = false;
-  if (lds > 65536 && !lds_set) {
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-      (void)hipGetLastError();
-      set_error("spectral: cannot reserve %zu B of LDS", lds);
-      return VQA_E_UNSUPPORTED;
-    }
-    lds_set = true;
-  }
-  static int cus = [] {
-    int dev = 0, v = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    return v;
-  }();
-  static int per_cu = [&] {
-    int v = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, 64 * W, lds) != hipSuccess || v <= 0) {
-      (void)hipGetLastError();
-      v = 1;
-    }
-    return v;
-  }();
-  const int npairs = (pa.B * pa.F + 1) / 2;
-  const int grid = std::min((npairs + W - 1) / W, cus * per_cu);
-  hipLaunchKernelGGL((spec_pairw_kernel<N, MODE>), dim3(grid), dim3(64 * W), lds, s, pa);
-  VQA_LAUNCHED("spec_pairw_kernel");
-  return VQA_OK;
-}
-
-// VQA_SPEC_IMPL=1: the one-wave-per-SIMD kernel (A/B); default: the two-waves-per-SIMD form
-static bool spec_use_w() {
-  static const bool w = [] {
-    const char* e = getenv("VQA_SPEC_IMPL");
-    return !(e && e[0] == '1');
-  }();
-  return w;
-}
-
 template <int MODE>
 static int dispatch_pairs(int n_fft, const SpecPairArgs& pa, hipStream_t s) {
-  if (spec_use_w()) {
-    switch (n_fft) {
-      case 256: return launch_pairsw<256, MODE>(pa, s);
-      case 512: return launch_pairsw<512, MODE>(pa, s);
-      case 1024: return launch_pairsw<1024, MODE>(pa, s);
-      case 2048: return launch_pairsw<2048, MODE>(pa, s);
-      default: break;
-    }
-  }
   switch (n_fft) {
     case 256: return launch_pairs<256, MODE>(pa, s);
     case 512: return launch_pairs<512, MODE>(pa, s);
@@ -1137,13 +824,6 @@ static int spec_loss(const float* tg, const float* r, float* loss_out, float* dr
   ga.B = B;
   ga.T = T;
   ga.nres = nres;
-  if (grad && T % 4 == 0 && ((uintptr_t)dr & 15) == 0 && spec_use_w()) {
-    long long nb = ((long long)B * T / 4 + 255) / 256;
-    if (nb > 8192) nb = 8192;
-    hipLaunchKernelGGL(spec_gather4_kernel, dim3((int)nb), dim3(256), 0, s, ga);
-    VQA_LAUNCHED("spec_gather4_kernel");
-    return VQA_OK;
-  }
   long long nb = grad ? ((long long)B * T + 255) / 256 : 1;
   if (nb > 8192) nb = 8192;
   hipLaunchKernelGGL(spec_gather_kernel, dim3((int)nb), dim3(256), 0, s, ga);
