@@ -161,11 +161,9 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
   const long long n0 = (long long)blockIdx.x * 256 + wave * 64;
 
   bf16x8 af[RT][KS];
-  float zq[RT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const long long row = n0 + rt * 16 + (lane & 15);
-    float s = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       bf16x8 v;
@@ -176,17 +174,31 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
         for (int j = 0; j < 8; ++j) v[j] = (bf16)0.f;
       }
       af[rt][ks] = v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (float)v[j];
-        s += f * f;
-      }
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(s, 4 * (lane >> 4) + r, 64);
   }
+  // |z|^2 of the rows this lane reports (row 4 (lane >> 4) + r of tile rt), from the A fragments: needed only by
+  // the epilogue, so it is evaluated there (16 fewer live registers in the code loop: 3 waves per SIMD)
+  auto row_sqnorms = [&](float (&zq)[RT][4]) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float s = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)af[rt][ks][j];
+          s += f * f;
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(s, 4 * (lane >> 4) + r, 64);
+    }
+  };
+#ifdef VQA_ARGMIN_DIST_FORM
+  float zq[RT][4];
+  row_sqnorms(zq);
+#endif
 
   // the kernel maximises key = z.e - |e|^2 / 2 (distance = |z|^2 - 2 key): the MFMA accumulator starts at
   // -|e|^2 / 2, so a code costs one compare and two selects per row (the distance form took an add and an fma
@@ -280,6 +292,10 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
     if (more) store_chunk(b ^ 1);  // buffer b ^ 1 was last read before the previous barrier
     __syncthreads();
   }
+#ifndef VQA_ARGMIN_DIST_FORM
+  float zq[RT][4];
+  row_sqnorms(zq);
+#endif
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
