@@ -51,6 +51,20 @@ class SpectralTarget:
         self.B, self.T = self.x.shape
         self.mags = V.spectral_target(self.x, *STFT_ARGS)
         self._ws = {}
+        # the spectrograms are complete when this event (on the producing stream) has fired: a loss on another
+        # stream waits for it (the levels' streams only need the target at their losses, not at their start)
+        self.ready = None
+        if self.x.is_cuda:
+            self._stream = torch.cuda.current_stream(self.x.device)
+            self.ready = torch.cuda.Event()
+            self.ready.record(self._stream)
+
+    def wait(self):
+        """Order the current stream after the spectrograms (no-op on the producing stream)."""
+        if self.ready is not None:
+            cur = torch.cuda.current_stream(self.x.device)
+            if cur != self._stream:
+                cur.wait_event(self.ready)
 
     def workspace(self, grad: bool) -> torch.Tensor:
         """Loss scratch, one per stream (levels on concurrent streams never share it)."""
@@ -72,6 +86,7 @@ def multispectral_loss_and_grad(target: SpectralTarget, recon: torch.Tensor, los
         raise ValueError(f"reconstruction {tuple(r.shape)} vs target {tuple(target.x.shape)}")
     loss = loss_out if loss_out is not None else torch.empty(1, dtype=torch.float32, device=r.device)
     dr = torch.empty_like(r) if need_grad else None
+    target.wait()
     V.spectral_loss_target(target.mags, r.contiguous(), loss, dr, None, *STFT_ARGS, ws=target.workspace(need_grad))
     return loss, (dr.reshape(recon.shape) if need_grad else None)
 

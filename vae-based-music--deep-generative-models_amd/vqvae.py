@@ -180,6 +180,9 @@ class VQVAE:
         # run the levels' independent forward/backward chains on one stream each (VQA_LEVEL_STREAMS=0: serial)
         self.concurrent_levels = os.environ.get("VQA_LEVEL_STREAMS", "1") != "0"
         self._streams = None
+        # A/B switch (VQA_STEP_LAYOUT=r3): the round-3 step layout — the target spectrograms on the producer stream
+        # before the levels fork, every level's codebook EMA after the join
+        self._r3_layout = os.environ.get("VQA_STEP_LAYOUT") == "r3"
 
     # ------------------------------------------------------------------ keras-like API
     def compile(self, optimizer=None, **kwargs):
@@ -226,19 +229,28 @@ class VQVAE:
 
     # ------------------------------------------------------------------ the step
     def _compute(self, x: torch.Tensor, training_grads: bool):
-        """Forward (+ backward when training_grads) of every level; EMA sums into the bucket."""
+        """Forward (+ backward when training_grads) of every level; EMA sums into the bucket. On one device the
+        codebook EMA of each level runs at the end of its own chain (only the bucket exchange needs it later)."""
         self._stats_region.zero_()
-        target = SpectralTarget(x)
         main = torch.cuda.current_stream(self.device)
         streams = self._level_streams()
-        for l in range(self.levels):
-            if streams is None:
-                self._level_step(x, l, target, training_grads)
-                continue
-            streams[l].wait_stream(main)
-            with torch.cuda.stream(streams[l]):
-                self._level_step(x, l, target, training_grads)
-        if streams is not None:
+        ema_in_level = self._world() == 1 and not self._r3_layout
+        if streams is None or self._r3_layout:
+            target = SpectralTarget(x)
+        if streams is None:
+            for l in range(self.levels):
+                self._level_step(x, l, target, training_grads, ema_in_level)
+        else:
+            for s in streams:
+                s.wait_stream(main)
+            # the target spectrograms (needed only by each level's loss) on level 0's stream, the shortest chain:
+            # the longer levels start their encoders at once and wait for the target at their losses
+            if not self._r3_layout:
+                with torch.cuda.stream(streams[0]):
+                    target = SpectralTarget(x)
+            for l in range(self.levels):
+                with torch.cuda.stream(streams[l]):
+                    self._level_step(x, l, target, training_grads, ema_in_level)
             for s in streams:
                 main.wait_stream(s)
         self.store.deferred = None
@@ -254,7 +266,7 @@ class VQVAE:
             self._streams = [torch.cuda.Stream(device=self.device) for _ in range(self.levels)]
         return self._streams
 
-    def _level_step(self, x, l, target, training_grads):
+    def _level_step(self, x, l, target, training_grads, ema=False):
         # this level's weight-gradient partials are reduced in one launch at its end
         self.store.deferred = V.Deferred() if training_grads else None
         enc, vq, dec = self.encoders[l], self.vqs[l], self.decoders[l]
@@ -269,16 +281,19 @@ class VQVAE:
         V.mse_loss(x, r, dr_spec, dr, self.loss_slots[l, 0:1])
         if training_grads:
             dq = dec.backward(dr)
-            dz = vq.backward(dq, n_global=n_loc)
+            dz = vq.backward(dq, n_global=n_loc)  # reads the codebook this step quantised with
             enc.backward(dz)
             self.store.deferred.flush()
+        if ema:
+            vq.apply_ema(update_trackers=False)  # after every use of the old codebook in this level
 
     def _update(self, apply_grads: bool):
         world = self._world()
         if apply_grads:
             self.optimizer.apply(self.store, grad_scale=1.0 / world)
-        for vq in self.vqs:
-            vq.apply_ema(update_trackers=False)
+        if world > 1 or self._r3_layout:  # on one device the levels' chains applied their EMA already (_compute)
+            for vq in self.vqs:
+                vq.apply_ema(update_trackers=False)
         # update_metrics (vqvae.py:262-304) + the VQ trackers: one launch
         V.step_metrics(self.loss_slots, self._vq_metrics, self._macc, self.levels, 1.0 / world)
 
