@@ -145,6 +145,44 @@ def test_quantize_commit_stats_backward(cuda, dt):
     assert torch.allclose(dz.cpu().float(), ref.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D", [32, 64, 16])
+def test_quantize_backward_vectorised_and_scalar_forms_agree(cuda, dt, D):
+    """vq_quantize / vq_backward take the 8-channel vectorised kernels for D = 32 / 64 on 16-byte aligned rows
+    and the scalar kernels otherwise (D = 16, or rows starting off a 16-byte boundary): the straight-through
+    output and dz are bitwise the same either way (same fp32 arithmetic per element), the commitment loss
+    within fp32 summation-order rounding, and both match the fp64 restatement."""
+    N, K, beta = 3001, 512, 0.25
+    g = torch.Generator().manual_seed(D)
+    z = torch.randn(N, D, generator=g).to(dt)
+    ET = torch.randn(K, D, generator=g)
+    idx = torch.randint(0, K, (N,), generator=g)
+    dq = torch.randn(N, D, generator=g).to(dt)
+    scale = 2 * beta / (N * D)
+    ETd, idxd = ET.cuda(), idx.cuda()
+    res = []
+    for off in (0, 1):  # off = 1: every row buffer starts one element past a 16-byte boundary
+        def place(t):
+            buf = torch.zeros(t.numel() + 8, dtype=t.dtype, device=cuda)
+            v = buf[off:off + t.numel()].view(t.shape)
+            v.copy_(t.cuda())
+            return v
+        zd, dqd = place(z), place(dq)
+        q, dz = place(torch.zeros_like(z)), place(torch.zeros_like(z))
+        commit = torch.zeros(1, device=cuda)
+        V.vq_quantize(zd, ETd, idxd, q, commit, None, None, beta)
+        V.vq_backward(dqd, zd, ETd, idxd, dz, scale)
+        res.append((q.cpu(), dz.cpu(), float(commit)))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    qref = ET[idx].double()
+    want = beta * float(((qref - z.double()) ** 2).mean())
+    for r in res:
+        assert abs(r[2] - want) < 1e-5 * want
+    assert torch.equal(res[0][0], (z.float() + (ET[idx] - z.float())).to(dt))
+    ref = (dq.float() + scale * (z.float() - ET[idx])).to(dt)
+    assert torch.allclose(res[0][1].float(), ref.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("N,K", [(20000, 2048), (100, 256), (1000, 1000)])
 def test_reset_rows_match_numpy_permutation(cuda, N, K):
     D = 8

@@ -62,7 +62,7 @@ template <class T, int LC>
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const T* x, const float* gamma, const float* beta, T* y,
                                                            long long rows, int C, float eps) {
   const int lane = threadIdx.x & 63;
-  for (long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long long)gridDim.x * 4) {
+  for (long long r = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); r < rows; r += (long long)gridDim.x * 4) {
     float xv[LC], mean, inv;
     ln_row_stats<T, LC>(x + r * C, C, xv, mean, inv, eps);
 #pragma unroll
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* x, const T*
                                                            float* part, long long rows, int C, float eps,
                                                            long long rows_per_wg) {
   extern __shared__ float red[];  // [4][2C]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float gg[LC], gb[LC];
 #pragma unroll
   for (int i = 0; i < LC; ++i) gg[i] = gb[i] = 0.f;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void layernorm8_fwd_kernel(const T* x, const f
 #pragma unroll
   for (int i = 0; i < 8; ++i) { gm[i] = gamma[c0 + i]; bt[i] = beta[c0 + i]; }
   const long long rstep = (long long)gridDim.x * 4 * RPW;
-  for (long long r = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub; r < rows; r += rstep) {
+  for (long long r = ((long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * RPW + sub; r < rows; r += rstep) {
     float v[8];
     ld8v(x + r * C + c0, v);
     float s = 0.f;
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void layernorm8_bwd_kernel(const T* x, const T
                                                             long long rows_per_wg) {
   constexpr int C = 8 * R, RPW = 64 / R;
   extern __shared__ float red[];  // [4][2C]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane / R, c0 = 8 * (lane % R);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), sub = lane / R, c0 = 8 * (lane % R);
   float gm[8], gg[8], gb[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { gm[i] = gamma[c0 + i]; gg[i] = gb[i] = 0.f; }

@@ -1240,7 +1240,7 @@ __device__ __forceinline__ float reduce_col16(const float* ws, int nparts, int E
 // per wave); the 8 per-thread sums, then the 4 waves, are combined in a fixed order: deterministic.
 constexpr int kRedCols256 = 256;
 __device__ __forceinline__ f32x4 reduce_col256(const float* ws, int nparts, int E, int e, f32x4 (*red)[64]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   f32x4 s[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) s[u] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -75,7 +75,7 @@ template <> __device__ __forceinline__ void dt_store8<float>(float* p, const flo
 constexpr int DT_COMP_WAVES = DT_NV + 2 * DT_C + 1;
 __global__ __launch_bounds__(256) void dtail_compose_kernel(const float* w_up, const float* b_up, const float* w_out,
                                                             const float* b_out, int Cu, float* comp) {
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (e >= DT_COMP_WAVES) return;
   if (e < DT_NV + 2 * DT_C) {
     float s = 0.f;
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
   const long long rows = (long long)a.B * a.T;
   constexpr int U = 4;  // row groups of 16 per wave and iteration, all loads issued first
   const long long step = (long long)gridDim.x * 64 * U;
-  for (long long R0 = (long long)blockIdx.x * 64 * U + (threadIdx.x >> 6) * 16 * U; R0 < rows; R0 += step) {
+  for (long long R0 = (long long)blockIdx.x * 64 * U + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 16 * U; R0 < rows; R0 += step) {
     Raw8<T> raw[U][3];
     int nn[U], jj[U];
     bool lv[U];
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
 template <class T>
 __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
   __shared__ float red[4][4][68];  // [wave][q][element of the lane's slice]
-  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float v[3][8][2], e0[8], e1[8];
 #pragma unroll
   for (int t = 0; t < 3; ++t)
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void dtail_chain_kernel(const float* red, cons
   auto sk = [&](int k) { return S - (k == 0 ? F : 0.f) - (k == 2 ? L : 0.f); };
   if ((int)blockIdx.x < nbo) {
     // dW_out[k][o] = sum_{a, p, c} dV_k[a][c][p] W_up[p + k - 2a][o][c] + b_up[o] S_k
-    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int e = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (e >= 3 * Cu) return;
     const int k = e / Cu, o = e % Cu;
     float x = 0.f;

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void seqlin_kernel(SeqLinArgs a) {
   const int halo = a.taps - 1, lo = a.dir < 0 ? halo : 0;
   T* X = Wt + a.N * KS;      // [kSlRows + halo][K + PAD]; row j <-> time t0 - lo + j
   const int seq = blockIdx.x / a.tiles_per_seq, t0 = (blockIdx.x - seq * a.tiles_per_seq) * kSlRows;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // stage the row tile (16-byte chunks; zeros outside the sequence)
   {
     constexpr int VEC = 16 / (int)sizeof(T);
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
   constexpr bool LE = TAPS == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Wt = (T*)smem;  // [TAPS * N][K + PAD]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, kof = M::koff(lane),
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), col = lane & 15, kof = M::koff(lane),
             g4 = 4 * (lane >> 4);
   const int ES = a.N + kSdEpad, cpr = a.N / VEC, nch = 16 * cpr;
   float* E = (float*)(Wt + TAPS * a.N * KS) + wave * 16 * ES;  // this wave's [16][N + pad] fp32 tile (LE)
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void seqlin_wgrad_kernel(SeqWgArgs a) {
   T* Y = X + (CH + halo) * XS;   // [CH][N + PAD]
   const int seq = blockIdx.x / a.segs_per_seq, seg = blockIdx.x - seq * a.segs_per_seq;
   const int tb = seg * a.seg_rows, te = std::min(a.T, tb + a.seg_rows);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int npairs = a.taps * (a.K / 16);
   f32x4 acc[PPW][NT], accb[NT];
 #pragma unroll
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) T Ks[64 * AKS];
   __shared__ __attribute__((aligned(16))) T Vs[64 * AKS];
   const int qt = blockIdx.x, h = blockIdx.y, n = blockIdx.z, q0 = qt * 64, b = q0 / a.l;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), li = lane & 15, g = lane >> 4;
   const int qi = q0 + wave * 16 + li;
   const long long qrow = (long long)n * a.T + qi;
   T* orow = (T*)a.o + (qrow * a.H + h) * AHD + 4 * g;
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) T Ks[64 * AKS];
   __shared__ __attribute__((aligned(16))) T Vs[64 * AKS];
   const int qt = blockIdx.x, h = blockIdx.y, n = blockIdx.z, q0 = qt * 64, b = q0 / a.l;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), li = lane & 15, g = lane >> 4;
   const int qi = q0 + wave * 16 + li;
   const long long qrow = (long long)n * a.T + qi, off = (qrow * a.H + h) * AHD;
   // D = rowsum(dO * O)
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ls[64];
   __shared__ __attribute__((aligned(16))) float Dd[64];
   const int kt = blockIdx.x, h = blockIdx.y, n = blockIdx.z, k0 = kt * 64, b = k0 / a.l;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), li = lane & 15, g = lane >> 4;
   const int ki = k0 + wave * 16 + li;
   const long long krow = (long long)n * a.T + ki, off = (krow * a.H + h) * AHD;
   T* dkrow = (T*)a.dk + off + 4 * g;
@@ -1205,7 +1205,7 @@ __device__ __forceinline__ float head_dot_row(const typename Mfma<T>::frag (&xf)
 template <class T>
 __device__ __forceinline__ void head_xfrags(typename Mfma<T>::frag (&xf)[2][HK / Mfma<T>::KS], const T* X, int stride) {
   typedef Mfma<T> M;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, kof = M::koff(lane), col = lane & 15;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), kof = M::koff(lane), col = lane & 15;
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   T* X = (T*)smem;     // [128][S]
   T* W = X + 128 * S;  // [64][S]
   const long long r0 = (long long)blockIdx.x * 128;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), li = lane & 15, g = lane >> 4;
   stage_rows128<T>(X, (const T*)a.x, r0, a.M, 128);
   Rows64Regs<T> wn;
   wn.load((const T*)a.wt, 0, a.V);
@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
   T* X = (T*)smem;
   T* W = X + 128 * S;
   const long long r0 = (long long)blockIdx.x * 128;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), li = lane & 15, g = lane >> 4;
   stage_rows128<T>(X, (const T*)a.x, r0, a.M, 128);
   Rows64Regs<T> wn;
   wn.load((const T*)a.wt, 0, a.V);
@@ -1409,7 +1409,7 @@ __global__ __launch_bounds__(256) void head_bwd_dw_kernel(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) int Tg[64];     // targets (-1 past the segment)
   const int nvt = (a.V + 63) / 64, vt = blockIdx.x % nvt, seg = blockIdx.x / nvt, v0 = vt * 64;
   const long long rb = (long long)seg * a.seg_rows, re = std::min<long long>(a.M, rb + a.seg_rows);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), li = lane & 15, g = lane >> 4;
   const int v = v0 + wave * 16 + li;
   constexpr float L2E = 1.4426950408889634f;
   const float bl = v < a.V ? a.bias[v] * L2E : -INFINITY;  // vocab slots past V: probability 0
@@ -1716,7 +1716,7 @@ __global__ __launch_bounds__(256) void prior_decode_kernel(DecArgs a) {
         }
         __syncthreads();
         // per head max and sum (wave h reduces head h)
-        const int wave = tid >> 6, lane = tid & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
         if (wave < a.H) {
           float m = -INFINITY;
           for (int idx = lane; idx < cnt; idx += 64) m = fmaxf(m, sc[wave][idx]);

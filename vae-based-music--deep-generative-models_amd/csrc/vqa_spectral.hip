@@ -405,7 +405,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f32x2* tw = (f32x2*)smem;
   float* wn = (float*)(tw + N);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   f32x2* z = (f32x2*)(wn + N) + (size_t)wave * fpad<N>();
 
   // twiddles, and the window zero-padded to N (the FFT's zero padding without a per-sample branch)

@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const f
   constexpr int KC = 128, DS = D / 4, RT = 2;
   __shared__ float El[D * KC];
   __shared__ float el2[KC];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const long long n0 = (long long)blockIdx.x * 128 + wave * 32;
 
   // A fragments: z[n0 + rt*16 + (lane&15)][4*ds + (lane>>4)]
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
   static_assert(KC * PPC % 256 == 0 && KC <= 256, "chunk staging");
   __shared__ __attribute__((aligned(16))) bf16 El[2][KC * CS];
   __shared__ float el2[2][KC];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const long long n0 = (long long)blockIdx.x * 256 + wave * 64;
 
   bf16x8 af[RT][KS];
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void vq_argmin_direct_kernel(const T* z, const
 // |e_k|^2, one wave per code: lane d squares e[d][k] (d, d + 64, ... for D > 64), then a butterfly sum over the
 // wave — the summation order of vq_ema_apply_kernel's fused |e|^2, so both give the same bits for the same E
 __global__ __launch_bounds__(256) void vq_sqnorm_kernel(const float* E, float* esq, int D, int K) {
-  const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (k >= K) return;  // wave-uniform
   float s = 0.f;
   for (int d = lane; d < D; d += 64) {
@@ -444,6 +444,52 @@ __global__ __launch_bounds__(256) void vq_backward_kernel(const T* dq, const T* 
   }
 }
 
+// Vectorised forms for D = 32 / 64 (the model's latent widths): a thread owns 8 consecutive channels of one row,
+// so z / dq / q_st / dz move in 16-byte (bf16) pieces, the row's code is one load per 8 channels, and the
+// element -> (row, channel) map is a shift of a 32-bit index instead of a 64-bit division per element. The
+// per-element arithmetic is the scalar kernels' (fp32, no contraction), so q_st and dz are bitwise the same;
+// the commitment partials are summed in another order (a float sum: within the tests' tolerance).
+template <class T, int D>
+__global__ __launch_bounds__(256) void vq_quantize8_kernel(const T* z, const float* ET, const int64_t* idx, T* qst,
+                                                          int N, float* ws) {
+  __shared__ float red[4];
+  constexpr int OPR = D / 8;  // 8-channel pieces per row
+  const int total = N * OPR;
+  float part = 0.f;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < total; o += gridDim.x * 256) {
+    const int n = o / OPR, c = (o - n * OPR) * 8;
+    const size_t e = (size_t)n * D + c;
+    const float* q = ET + idx[n] * D + c;
+    const f32x4 z0 = ld4(z + e), z1 = ld4(z + e + 4);
+    const f32x4 d0 = *(const f32x4*)q - z0, d1 = *(const f32x4*)(q + 4) - z1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part += d0[i] * d0[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part += d1[i] * d1[i];
+    st4(qst + e, z0 + d0);
+    st4(qst + e + 4, z1 + d1);
+  }
+  const float s = block_sum_256(part, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+template <class T, int D>
+__global__ __launch_bounds__(256) void vq_backward8_kernel(const T* dq, const T* z, const float* ET,
+                                                          const int64_t* idx, T* dz, float scale, int N) {
+  constexpr int OPR = D / 8;
+  const int total = N * OPR;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < total; o += gridDim.x * 256) {
+    const int n = o / OPR, c = (o - n * OPR) * 8;
+    const size_t e = (size_t)n * D + c;
+    const float* q = ET + idx[n] * D + c;
+    const f32x4 z0 = ld4(z + e), z1 = ld4(z + e + 4);
+    const f32x4 g0 = ld4(dq + e), g1 = ld4(dq + e + 4);
+    const f32x4 t0 = z0 - *(const f32x4*)q, t1 = z1 - *(const f32x4*)(q + 4);
+    st4(dz + e, g0 + scale * t0);
+    st4(dz + e + 4, g1 + scale * t1);
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void vq_reset_rows_kernel(const T* z, float* RT, long long N_local,
                                                            long long row_offset, long long N_global, int D, int K,
@@ -466,7 +512,7 @@ __global__ __launch_bounds__(256) void vq_ema_apply_kernel(float* E, float* ET, 
                                                           const float* m_sumT, const float* n_sum, const float* RT,
                                                           float g, float omg, float thresh, int64_t* counter,
                                                           float* esq, bf16* E3, int D, int K) {
-  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int d = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;
   if (k >= K) return;  // wave-uniform
@@ -534,6 +580,15 @@ static int quantize_blocks(long long total) {
   return (int)b;
 }
 
+// the vectorised forms apply: D = 32 / 64, 16-byte aligned rows, 32-bit piece indices
+static bool vq_vec8_ok(long long N, int D, std::initializer_list<const void*> ptrs) {
+  if ((D != 32 && D != 64) || N * (D / 8) >= (1ll << 31)) return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16) return false;
+  return true;
+}
+static int vec8_blocks(long long N, int D) { return quantize_blocks(N * D / 8); }
+
 // ---- EMA sums by code (VectorQuantizer.py:123-124: m_sum = z^T onehot, n_sum = column sums of onehot) ----
 // Deterministic: the rows are counting-sorted by code (stable: by code, then row), and every code's sum is
 // taken over its rows in that order — sequential runs within 64-position tiles, tile partials added in tile
@@ -583,23 +638,24 @@ static SortWs sort_ws(void* base, long long N, int D, int K) {
 
 __global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t* idx, SortWs w, int N, int K) {
   extern __shared__ int hist[];  // [K]
-  __shared__ __attribute__((aligned(16))) int codes[kSortChunk];
-  const int c = blockIdx.x, tid = threadIdx.x, row = c * kSortChunk + tid;
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, row = c * kSortChunk + tid;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t v = row < N ? idx[row] : -1;
   const int k = (v >= 0 && v < K) ? (int)v : -1;  // an index outside [0, K) contributes to no code
-  codes[tid] = k;
   for (int i = tid; i < K; i += kSortChunk) hist[i] = 0;
-  __syncthreads();
-  // stable rank: equal codes at lower rows of the chunk (wave-uniform trip count, 4 codes per LDS read)
-  const int wend = ((tid >> 6) + 1) * 64;
+  // stable rank = equal codes at lower lanes of the row's wave + equal codes in the chunk's earlier waves
   int r = 0;
-  for (int j = 0; j < wend; j += 4) {
-    const int4 q = *(const int4*)(codes + j);
-    r += (q.x == k && j < tid) + (q.y == k && j + 1 < tid) + (q.z == k && j + 2 < tid) + (q.w == k && j + 3 < tid);
-  }
-  if (k >= 0) {
-    w.lrank[row] = r;
-    atomicAdd(hist + k, 1);  // integer: order-independent
+#pragma unroll
+  for (int j = 0; j < 63; ++j) r += (__builtin_amdgcn_readlane(k, j) == k) & (j < lane);
+  // the waves take turns in row order: read the running histogram (the earlier waves' counts), then add
+  // their own rows (integer LDS atomics; a wave's read completes before its adds are issued)
+  for (int t = 0; t < kSortChunk / 64; ++t) {
+    __syncthreads();
+    if (wv == t && k >= 0) {
+      r += hist[k];
+      w.lrank[row] = r;
+      atomicAdd(hist + k, 1);
+    }
   }
   __syncthreads();
   for (int i = tid; i < K; i += kSortChunk) w.cnt[(size_t)c * K + i] = hist[i];
@@ -609,7 +665,7 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t
 // prefixed in LDS, then each wave writes its range's exclusive offsets
 __global__ __launch_bounds__(1024) void vq_sort_scan_kernel(SortWs w, float* n_sum, int nch, int K) {
   __shared__ int part[16][64];
-  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6, k = blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x & 63, v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), k = blockIdx.x * 64 + lane;
   const int per = (nch + 15) / 16, c0 = min(nch, v * per), c1 = min(nch, c0 + per);
   int s = 0;
   if (k < K)
@@ -642,7 +698,7 @@ __global__ __launch_bounds__(1024) void vq_sort_scan_kernel(SortWs w, float* n_s
 // exclusive scan of tot[0..K) into seg (LDS, K + 1 ints) by the block's 1024 threads
 __device__ void seg_scan(const int* tot, int* seg, int K) {
   __shared__ int wsum[16];
-  const int tid = threadIdx.x, lane = tid & 63, v = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, v = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int per = (K + kSortChunk - 1) / kSortChunk, i0 = min(K, tid * per), i1 = min(K, i0 + per);
   int s = 0;
   for (int i = i0; i < i1; ++i) s += tot[i];
@@ -683,21 +739,25 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_scatter_kernel(const int64
 template <class T>
 __global__ __launch_bounds__(256) void vq_seg_sum_kernel(const T* z, SortWs w, float* m_sumT, int K, int D) {
   const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform tile (readfirstlane): np and the run bookkeeping stay scalar, and the 64 row loads below are
+  // unconditional, so they are all in flight at once (a per-lane `i < np` guard made the compiler wrap each
+  // load in its own branch and wait on it: 64 serialised HBM round trips per wave)
+  const int tile = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p0 = tile * kSegTile;
   const int N = w.seg[K];  // sorted positions = rows with a valid code
   if (p0 >= N) return;
   const int np = min(kSegTile, N - p0);
-  const int myrow = lane < np ? w.perm[p0 + lane] : 0;
+  const int myrow = w.perm[p0 + min(lane, np - 1)];  // positions past np repeat a valid row (never summed)
   const int mycode = lane < np ? w.scode[p0 + lane] : -1;
   for (int d0 = 0; d0 < D; d0 += 64) {
     const int d = d0 + lane;
     const bool on = d < D;
+    const int dl = min(d, D - 1);
     float v[kSegTile];
 #pragma unroll
     for (int i = 0; i < kSegTile; ++i) {
       const int row = __builtin_amdgcn_readlane(myrow, i);
-      v[i] = (on && i < np) ? ld(z + (size_t)row * D + d) : 0.f;
+      v[i] = ld(z + (size_t)row * D + dl);
     }
     float s = 0.f;
     int a = 0;
@@ -725,7 +785,7 @@ __global__ __launch_bounds__(256) void vq_seg_sum_kernel(const T* z, SortWs w, f
 // the tile range in order, then the quarters are added in order (a fixed tree for a given segment)
 __global__ __launch_bounds__(256) void vq_seg_combine_kernel(SortWs w, float* m_sumT, int D) {
   __shared__ float q[4][64];
-  const int k = blockIdx.x, lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int k = blockIdx.x, lane = threadIdx.x & 63, v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int S = w.seg[k], E = w.seg[k + 1];
   if (E <= S) return;
   const int ta = S / kSegTile, tb = (E - 1) / kSegTile;
@@ -733,11 +793,18 @@ __global__ __launch_bounds__(256) void vq_seg_combine_kernel(SortWs w, float* m_
   const int n = tb - ta;  // tiles ta+1 .. tb read tfirst
   const int per = (n + 3) / 4, i0 = ta + 1 + min(n, v * per), i1 = ta + 1 + min(n, (v + 1) * per);
   for (int d0 = 0; d0 < D; d0 += 64) {
-    const int d = d0 + lane;
+    const int d = d0 + lane, dl = min(d, D - 1);
     float s = 0.f;
-    if (d < D) {
-      if (v == 0) s = (S == ta * kSegTile ? w.tfirst : w.tlast)[(size_t)ta * D + d];
-      for (int t = i0; t < i1; ++t) s += w.tfirst[(size_t)t * D + d];
+    if (v == 0) s = (S == ta * kSegTile ? w.tfirst : w.tlast)[(size_t)ta * D + dl];
+    // 8 tile partials in flight per wave (clamped indices, unconditional loads), added in tile order: the
+    // same sum as one load-add at a time, without a full HBM round trip per tile of a long segment
+    for (int t = i0; t < i1; t += 8) {
+      float u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = w.tfirst[(size_t)min(t + j, i1 - 1) * D + dl];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (t + j < i1) s += u[j];
     }
     q[v][lane] = s;
     __syncthreads();
@@ -860,14 +927,34 @@ extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* id
           (long long)N, D, K);
   VQA_ARG(workspace && ws_bytes >= vqa_vq_quantize_workspace(N, D, K, dtype), "vq_quantize: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  // q, straight-through output and the commitment partials
-  if (dtype == VQA_BF16)
-    hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st,
-                       (long long)N, D, (float*)workspace);
-  else
-    hipLaunchKernelGGL(vq_quantize_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)z, ET, idx, (float*)q_st,
-                       (long long)N, D, (float*)workspace);
-  VQA_LAUNCHED("vq_quantize_kernel");
+  // q, straight-through output and the commitment partials (nparts <= nb: the workspace's partial rows)
+  int nparts = nb;
+  if (vq_vec8_ok(N, D, {z, ET, q_st})) {
+    nparts = vec8_blocks(N, D);
+    float* ws = (float*)workspace;
+    const int n = (int)N;
+    if (dtype == VQA_BF16 && D == 64)
+      hipLaunchKernelGGL((vq_quantize8_kernel<bf16, 64>), dim3(nparts), dim3(256), 0, s, (const bf16*)z, ET, idx,
+                         (bf16*)q_st, n, ws);
+    else if (dtype == VQA_BF16)
+      hipLaunchKernelGGL((vq_quantize8_kernel<bf16, 32>), dim3(nparts), dim3(256), 0, s, (const bf16*)z, ET, idx,
+                         (bf16*)q_st, n, ws);
+    else if (D == 64)
+      hipLaunchKernelGGL((vq_quantize8_kernel<float, 64>), dim3(nparts), dim3(256), 0, s, (const float*)z, ET, idx,
+                         (float*)q_st, n, ws);
+    else
+      hipLaunchKernelGGL((vq_quantize8_kernel<float, 32>), dim3(nparts), dim3(256), 0, s, (const float*)z, ET, idx,
+                         (float*)q_st, n, ws);
+    VQA_LAUNCHED("vq_quantize8_kernel");
+  } else {
+    if (dtype == VQA_BF16)
+      hipLaunchKernelGGL(vq_quantize_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)z, ET, idx, (bf16*)q_st,
+                         (long long)N, D, (float*)workspace);
+    else
+      hipLaunchKernelGGL(vq_quantize_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)z, ET, idx, (float*)q_st,
+                         (long long)N, D, (float*)workspace);
+    VQA_LAUNCHED("vq_quantize_kernel");
+  }
   if (m_sumT) {
     void* sws = (char*)workspace + align256((size_t)nb * sizeof(float));
     const int rc = dtype == VQA_BF16
@@ -877,7 +964,7 @@ extern "C" int vqa_vq_quantize(const void* z, const float* ET, const int64_t* id
   }
   // beta * mean((q - z)^2) over N*D elements (VectorQuantizer.py:97-99)
   const float scale = (float)((double)beta / ((double)N * (double)D));
-  hipLaunchKernelGGL(reduce_scalar_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, scale, commit_out);
+  hipLaunchKernelGGL(reduce_scalar_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nparts, scale, commit_out);
   VQA_LAUNCHED("reduce_scalar_kernel");
   return VQA_OK;
 }
@@ -887,6 +974,23 @@ extern "C" int vqa_vq_backward(const void* dq, const void* z, const float* ET, c
   VQA_ARG(dq && z && ET && idx && dz && N > 0 && D > 0, "vq_backward: bad arguments");
   const int nb = quantize_blocks((long long)N * D);
   hipStream_t s = (hipStream_t)stream;
+  if ((dtype == VQA_BF16 || dtype == VQA_F32) && vq_vec8_ok(N, D, {dq, z, ET, dz})) {
+    const int g = vec8_blocks(N, D), n = (int)N;
+    if (dtype == VQA_BF16 && D == 64)
+      hipLaunchKernelGGL((vq_backward8_kernel<bf16, 64>), dim3(g), dim3(256), 0, s, (const bf16*)dq, (const bf16*)z,
+                         ET, idx, (bf16*)dz, scale, n);
+    else if (dtype == VQA_BF16)
+      hipLaunchKernelGGL((vq_backward8_kernel<bf16, 32>), dim3(g), dim3(256), 0, s, (const bf16*)dq, (const bf16*)z,
+                         ET, idx, (bf16*)dz, scale, n);
+    else if (D == 64)
+      hipLaunchKernelGGL((vq_backward8_kernel<float, 64>), dim3(g), dim3(256), 0, s, (const float*)dq,
+                         (const float*)z, ET, idx, (float*)dz, scale, n);
+    else
+      hipLaunchKernelGGL((vq_backward8_kernel<float, 32>), dim3(g), dim3(256), 0, s, (const float*)dq,
+                         (const float*)z, ET, idx, (float*)dz, scale, n);
+    VQA_LAUNCHED("vq_backward8_kernel");
+    return VQA_OK;
+  }
   if (dtype == VQA_BF16)
     hipLaunchKernelGGL(vq_backward_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)dq, (const bf16*)z, ET, idx,
                        (bf16*)dz, scale, (long long)N, D);
