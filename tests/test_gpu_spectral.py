@@ -119,3 +119,29 @@ def test_shared_target(cuda, B, T):
         assert abs(float(l1) - loss_ref) / loss_ref < 1e-5
         err = (g1.cpu().double() - g_ref).abs().max() / g_ref.abs().max()
         assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("args", [
+    [(512, 256), (20, 64), (300, 256)],                 # 15 frames over a sample: the general overlap-add
+    [(2048, 1024, 512, 256, 512), (240, 120, 50, 64, 100), (1200, 600, 240, 256, 300)],  # 5 resolutions
+    [(256,), (1,), (7,)],                                # hop 1
+    [tuple(a) for a in STFT_ARGS],                       # the model's: the 8-frame gather
+])
+def test_gradient_overlap_add_forms(cuda, args):
+    """The frame-gradient overlap-add runs as spec_gather8_kernel (<= 4 resolutions, <= 8 frames over a
+    sample) or spec_gather_kernel (otherwise); both against the fp64 autograd oracle for these resolutions."""
+    n_fft, hop, win = (list(a) for a in args)
+    B, T = 2, 4096 + 77
+    x, r = _signals(B, T, seed=len(n_fft) * 31 + hop[0])
+    rd = r.double().squeeze(-1).clone().requires_grad_(True)
+    xd = x.double().squeeze(-1)
+    per = torch.stack([R.norm(R.spectral(xd, n, h, w) - R.spectral(rd, n, h, w)) / R.norm(R.spectral(xd, n, h, w))
+                       for n, h, w in zip(n_fft, hop, win)], dim=-1).mean(dim=-1)
+    (g_ref,) = torch.autograd.grad(per.mean(), rd)
+    out = torch.empty(1, device=cuda)
+    dr = torch.empty(B, T, device=cuda)
+    V.spectral_loss(x.squeeze(-1).to(cuda).contiguous(), r.squeeze(-1).to(cuda).contiguous(), out, dr, None,
+                    n_fft, hop, win)
+    assert abs(float(out) - float(per.mean())) / float(per.mean()) < 1e-5
+    err = (dr.cpu().double() - g_ref).abs().max() / g_ref.abs().max()
+    assert err < 1e-4, err
