@@ -34,7 +34,7 @@ import torch  # noqa: E402
 
 import dp_worker as W  # noqa: E402
 
-CONFIG, DTYPE = "cfg2_short", "bf16"
+CONFIG, DTYPE = os.environ.get("VQA_DIAG_CONFIG", "cfg2_short"), os.environ.get("VQA_DIAG_DTYPE", "bf16")
 
 
 def worker(path, mode, out):
@@ -79,23 +79,63 @@ def worker(path, mode, out):
         return world
 
     vqa_dp.exchange = diag
+    import vqvae as VV
+    lrec = []
+    orig_msl = VV.multispectral_loss_and_grad
+
+    def msl(target, r_, loss_out=None, need_grad=True):
+        out = orig_msl(target, r_, loss_out=loss_out, need_grad=need_grad)
+        if len(lrec) < 3 and need_grad:  # the first step's three levels
+            rec = {"r": r_.detach().clone(), "dr": out[1].detach().clone(), "x": target.x.detach().clone()}
+            # the same loss again on the same inputs, in this process (is the spectral kernel chain repeatable
+            # while the other rank shares the GPU?), and a checksum of the target spectrograms
+            again = orig_msl(target, r_, loss_out=torch.empty(1, device=r_.device), need_grad=True)
+            rec["dr_again"] = again[1].detach().clone()
+            rec["mags_sum"] = target.mags.view(torch.int32).to(torch.int64).sum().reshape(1)
+            lrec.append(rec)
+        return out
+
+    VV.multispectral_loss_and_grad = msl
     res = W.run(m, xs, mode)
+    torch.cuda.synchronize()
+    r_levels = [{k: v.cpu() for k, v in d.items()} for d in lrec]
     r = rec[0]
     r["step1"] = torch.cat([res["step1"]["grads"], res["step1"]["stats"]])
     r["P"] = P
+    r["levels"] = r_levels
+    r["stats_regions"] = [(int(a), int(b)) for a, b in m.layout["stats"]]
+    r["KD"] = (m.vqs[0].num_embeddings if hasattr(m.vqs[0], "num_embeddings") else 0,
+               m.vqs[0].embedding_dim if hasattr(m.vqs[0], "embedding_dim") else 0)
     r["offsets"] = {k: (int(o), int(torch.Size(sh).numel())) for k, (o, sh) in m.store.offsets.items()}
     torch.save(r, out)
     dist.barrier()
     dist.destroy_process_group()
 
 
+REF_LEVELS = []
+
+
 def reference():
+    import vqvae as VV
     refs = []
+    orig_msl = VV.multispectral_loss_and_grad
     for r in range(2):
         m = W.build(W.B_LOCAL, config=CONFIG, dtype=DTYPE)
         x = m._as_input(W.batches(2, CONFIG)[0][r * W.B_LOCAL:(r + 1) * W.B_LOCAL])
+        lrec = []
+
+        def msl(target, r_, loss_out=None, need_grad=True):
+            out = orig_msl(target, r_, loss_out=loss_out, need_grad=need_grad)
+            if len(lrec) < 3 and need_grad:
+                lrec.append({"r": r_.detach().clone(), "dr": out[1].detach().clone(), "x": target.x.detach().clone(),
+                             "mags_sum": target.mags.view(torch.int32).to(torch.int64).sum().reshape(1)})
+            return out
+
+        VV.multispectral_loss_and_grad = msl
         m._compute(x, True)
         torch.cuda.synchronize()
+        VV.multispectral_loss_and_grad = orig_msl
+        REF_LEVELS.append([{k: v.cpu() for k, v in d.items()} for d in lrec])
         refs.append(m.bucket.detach().cpu().clone())
         del m
     torch.cuda.empty_cache()
@@ -144,6 +184,50 @@ def main():
                    "final!=sum": int((g["final"] != want).sum()),
                    "final!=after": int((g["final"] != g["after"]).sum()),
                    "step1!=final": int((g["step1"] != g["final"]).sum())}
+            # the level statistics at exchange entry (this rank's own m_sumT, n_sum, RT) vs one process: a code
+            # count that differs means the argmin (or its input z) differed
+            K, D = g["KD"]
+            sd = []
+            for l, (a, b) in enumerate(g["stats_regions"]):
+                got, ref = g["before"][a:b], refs[r][a:b]
+                if K and D:
+                    n_got, n_ref = got[K * D:K * D + K], ref[K * D:K * D + K]
+                    sd.append({"level": l, "m_sum!=": int((got[:K * D] != ref[:K * D]).sum()),
+                               "counts!=": int((n_got != n_ref).sum()),
+                               "rows_moved": float((n_got - n_ref).abs().sum()) / 2,
+                               "RT!=": int((got[K * D + K:] != ref[K * D + K:]).sum())})
+            chk["stats"] = sd
+            # per level: the reconstruction r, the spectral-loss gradient, the target waveform (rank vs one process)
+            lv = []
+            for a, b in zip(g["levels"], REF_LEVELS[r]):
+                e = dict({k: int((a[k] != b[k]).sum()) for k in b}, dr_repeat=int((a["dr_again"] != a["dr"]).sum()))
+                d = (a["r"].double() - b["r"].double()).reshape(a["r"].shape[0], -1)
+                if e["r"]:
+                    nz = d.nonzero()
+                    e["r_maxdiff"] = float(d.abs().max())
+                    e["r_maxval"] = float(b["r"].abs().max())
+                    e["r_where"] = [(int(i), int(t)) for i, t in nz[:12]]
+                lv.append(e)
+            chk["levels"] = lv
+            if n_loc:
+                dl = (g["before"][:P].double() - refs[r][:P].double()).abs()
+                chk["before_where"] = where(torch.cat([dl, torch.zeros(g["before"].numel() - P, dtype=dl.dtype)]),
+                                            g["offsets"], P)
+                # the parameters whose gradient differs, in forward order of the layers (first = most upstream)
+                chk["before_params"] = [nm for nm, (o, k) in sorted(g["offsets"].items(), key=lambda t: t[1][0])
+                                        if float(dl[o:o + k].max()) > 0][:12]
+                # per top-level module: differing / all parameters, and the differing ones in layout order
+                groups = {}
+                for nm, (o, k) in sorted(g["offsets"].items(), key=lambda t: t[1][0]):
+                    top = nm.split("/")[0]
+                    dif = float(dl[o:o + k].max()) > 0
+                    gr = groups.setdefault(top, [0, 0, []])
+                    gr[0] += dif
+                    gr[1] += 1
+                    if dif:
+                        gr[2].append(nm[len(top) + 1:] + f"({float(dl[o:o + k].max()):.0e})")
+                chk["groups"] = {t: f"{a}/{b}" for t, (a, b, _) in groups.items()}
+                chk["group_params"] = {t: lst for t, (a, b, lst) in groups.items() if a}
             if "staged" in g:
                 chk["staged!=before"] = int((g["staged"] != g["before"]).sum())
             if chk["after!=sum"]:

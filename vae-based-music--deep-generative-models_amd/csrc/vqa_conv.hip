@@ -1035,7 +1035,7 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* v)
 
 template <class TX, class TG, bool WIDE_X>
 __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
-  constexpr int KM = 4, NM = 2, U = 4;  // max taps, max narrow width, rows in flight per thread
+  constexpr int KM = 4, NM = 2, U = 8;  // max taps, max narrow width, rows in flight per thread
   const int W = WIDE_X ? a.C : a.O;
   const int NN = WIDE_X ? a.O : a.C;
   const int VL = W / 8, RL = 256 / VL;

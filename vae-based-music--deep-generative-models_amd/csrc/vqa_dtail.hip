@@ -31,6 +31,11 @@ template <class T> struct Raw8;
 template <> struct Raw8<bf16> {
   uint4 w;
   __device__ __forceinline__ void load(const bf16* p, bool ok) { w = ok ? *(const uint4*)p : uint4{0u, 0u, 0u, 0u}; }
+  // unconditional load (p must be valid), zeros selected when !ok
+  __device__ __forceinline__ void load_sel(const bf16* p, bool ok) {
+    const uint4 x = *(const uint4*)p;
+    w = uint4{ok ? x.x : 0u, ok ? x.y : 0u, ok ? x.z : 0u, ok ? x.w : 0u};
+  }
   __device__ __forceinline__ void get(float (&v)[8]) const {
     const unsigned u[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -48,6 +53,11 @@ template <> struct Raw8<float> {
       a = *(const f32x4*)p;
       b = *(const f32x4*)(p + 4);
     }
+  }
+  __device__ __forceinline__ void load_sel(const float* p, bool ok) {
+    const f32x4 x = *(const f32x4*)p, y = *(const f32x4*)(p + 4), z = {0.f, 0.f, 0.f, 0.f};
+    a = ok ? x : z;
+    b = ok ? y : z;
   }
   __device__ __forceinline__ void get(float (&v)[8]) const {
 #pragma unroll
@@ -122,7 +132,7 @@ struct DtArgs {
   int B, T;
 };
 
-// y[n, 2j + p] for 16 rows per wave and iteration (grid-stride over the B*T rows)
+// y[n, 2j + p] for 16 rows per wave and iteration; grid (row blocks, items), grid-stride over the item's rows
 template <class T>
 __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
   const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3;
@@ -139,28 +149,25 @@ __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
     e1[i] = a.comp[DT_NV + DT_C + 8 * q + i];
   }
   const float bias = a.comp[DT_NV + 2 * DT_C], b0 = a.comp[DT_NV + 2 * DT_C + 1], b2 = a.comp[DT_NV + 2 * DT_C + 2];
-  const T* H = (const T*)a.h;
-  const long long rows = (long long)a.B * a.T;
-  constexpr int U = 4;  // row groups of 16 per wave and iteration, all loads issued first
-  const long long step = (long long)gridDim.x * 64 * U;
-  for (long long R0 = (long long)blockIdx.x * 64 * U + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 16 * U; R0 < rows; R0 += step) {
+  const T* H = (const T*)a.h + (size_t)blockIdx.y * a.T * DT_C;  // item n = blockIdx.y
+  float* Y = a.y + (size_t)blockIdx.y * a.T * 2;
+  constexpr int U = 3;  // row groups of 16 per wave and iteration, all loads issued first (3: 136 VGPRs, 3 waves/SIMD)
+  const int step = gridDim.x * 64 * U;
+  for (int J0 = blockIdx.x * 64 * U + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 16 * U; J0 < a.T;
+       J0 += step) {
     Raw8<T> raw[U][3];
-    int nn[U], jj[U];
-    bool lv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long R = R0 + 16 * u + r;
-      lv[u] = R < rows;
-      nn[u] = lv[u] ? (int)(R / a.T) : 0;
-      jj[u] = lv[u] ? (int)(R - (long long)nn[u] * a.T) : 0;
-      const T* hr = H + ((long long)nn[u] * a.T + jj[u]) * DT_C + 8 * q;
-      raw[u][0].load(hr - DT_C, lv[u] && jj[u] > 0);
-      raw[u][1].load(hr, lv[u]);
-      raw[u][2].load(hr + DT_C, lv[u] && jj[u] + 1 < a.T);
+      const int j = J0 + 16 * u + r;
+      const bool lv = j < a.T;
+      const T* hr = H + (size_t)j * DT_C + 8 * q;
+      raw[u][0].load(hr - DT_C, lv && j > 0);
+      raw[u][1].load(hr, lv);
+      raw[u][2].load(hr + DT_C, lv && j + 1 < a.T);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int n = nn[u], j = jj[u];
+      const int j = J0 + 16 * u + r;
       float hm[8], h0[8], hp[8];
       raw[u][0].get(hm);
       raw[u][1].get(h0);
@@ -179,10 +186,10 @@ __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
       y1 += __shfl_xor(y1, 1, 64);
       y0 += __shfl_xor(y0, 2, 64);
       y1 += __shfl_xor(y1, 2, 64);
-      if (lv[u] && q == 0) {
+      if (j < a.T && q == 0) {
         y0 += bias - (j == 0 ? b0 : 0.f);
         y1 += bias - (j == a.T - 1 ? b2 : 0.f);
-        *(float2*)(a.y + ((long long)n * a.T + j) * 2) = make_float2(y0, y1);
+        *(float2*)(Y + (size_t)j * 2) = make_float2(y0, y1);
       }
     }
   }
@@ -212,37 +219,45 @@ __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
     for (int i = 0; i < 8; ++i) dv[t][i][0] = dv[t][i][1] = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) eh[i] = et[i] = 0.f;
-  const T* H = (const T*)a.h;
-  T* DH = (T*)a.dh;
-  const long long rows = (long long)a.B * a.T;
-  const long long step = (long long)gridDim.x * (blockDim.x >> 2);
+  const T* H = (const T*)a.h + (size_t)blockIdx.y * a.T * DT_C;  // item n = blockIdx.y
+  T* DH = (T*)a.dh + (size_t)blockIdx.y * a.T * DT_C;
+  const float* dyn = a.dy + (size_t)blockIdx.y * 2 * a.T;
   const int T2 = 2 * a.T;
   constexpr int U = 2;
-  for (long long R0 = (long long)blockIdx.x * 64 * U + wave * 16 * U; R0 < rows; R0 += step * U) {
-    Raw8<T> raw[U];
-    float g[U][6];  // dy[2j - 2 .. 2j + 3] (zero outside the item)
-    int nn[U], jj[U];
-    bool lv[U];
+  const int step = gridDim.x * 64 * U;
+  // the next iteration's h / dy loads are issued before this iteration's arithmetic (software pipelining: at two
+  // waves per SIMD the loads of one iteration alone cannot cover the HBM latency)
+  auto fetch = [&](int J, Raw8<T>(&raw)[U], float (&g)[U][6]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long R = R0 + 16 * u + r;
-      lv[u] = R < rows;
-      nn[u] = lv[u] ? (int)(R / a.T) : 0;
-      jj[u] = lv[u] ? (int)(R - (long long)nn[u] * a.T) : 0;
-      const float* dyn = a.dy + (long long)nn[u] * T2;
+      // unconditional loads from clamped addresses, zeros selected afterwards: no load sits in a branch, so the
+      // compiler's wait before the arithmetic counts only the previous iteration's loads, not these
+      const int j = J + 16 * u + r;
+      const bool lv = j < a.T;
+      const int jc = lv ? j : a.T - 1;
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
-        const int t = 2 * jj[u] - 2 + 2 * m;
-        float2 w = make_float2(0.f, 0.f);
-        if (lv[u] && t >= 0 && t < T2) w = *(const float2*)(dyn + t);
-        g[u][2 * m] = w.x;
-        g[u][2 * m + 1] = w.y;
+        const int t = 2 * j - 2 + 2 * m;
+        const bool ok = lv && t >= 0 && t < T2;
+        const float2 w = *(const float2*)(dyn + min(max(t, 0), T2 - 2));
+        g[u][2 * m] = ok ? w.x : 0.f;
+        g[u][2 * m + 1] = ok ? w.y : 0.f;
       }
-      raw[u].load(H + ((long long)nn[u] * a.T + jj[u]) * DT_C + 8 * q, lv[u]);
+      raw[u].load_sel(H + (size_t)jc * DT_C + 8 * q, lv);
     }
+  };
+  int J0 = blockIdx.x * 64 * U + wave * 16 * U;
+  Raw8<T> raw[U];
+  float g[U][6];  // dy[2j - 2 .. 2j + 3] (zero outside the item)
+  fetch(J0, raw, g);
+  for (; J0 < a.T; J0 += step) {
+    Raw8<T> rawn[U];
+    float gn[U][6];
+    fetch(J0 + step, rawn, gn);  // past the item: every lane's loads are predicated off (zeros)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int n = nn[u], j = jj[u];
+      const int j = J0 + 16 * u + r;
+      const bool lv = j < a.T;
       const float* gg = g[u];
       float h0[8];
       raw[u].get(h0);
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
         if (j == 0) d[i] -= e0[i] * gg[2];
         if (j == a.T - 1) d[i] -= e1[i] * gg[3];
       }
-      if (lv[u]) dt_store8<T>(DH + ((long long)n * a.T + j) * DT_C + 8 * q, d);
+      if (lv) dt_store8<T>(DH + (size_t)j * DT_C + 8 * q, d);
       // dV[a][c][p] = sum_j h[j + a][c] dy[2j + p] = sum_j h[j][c] dy[2(j - a) + p]: row j's own h against the
       // same dy window (out-of-item dy reads are zero); edge sums; dy sums (q == 0 lanes only)
 #pragma unroll
@@ -269,11 +284,17 @@ __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
         if (j == 0) eh[i] += h0[i] * gg[2];
         if (j == a.T - 1) et[i] += h0[i] * gg[3];
       }
-      if (q == 0 && lv[u]) {
+      if (q == 0 && lv) {
         sS += gg[2] + gg[3];
         if (j == 0) sF += gg[2];
         if (j == a.T - 1) sL += gg[3];
       }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      raw[u] = rawn[u];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g[u][k] = gn[u][k];
     }
   }
   // per-lane slice (64 values: dv 48 | eh 8 | et 8; q == 0 adds S, F, L) -> sum over the 16 rows of the
@@ -308,7 +329,7 @@ __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
     for (int e = 0; e < 67; ++e) red[wave][q][e] = s[e];
   }
   __syncthreads();
-  float* out = a.part + (size_t)blockIdx.x * DT_PART;
+  float* out = a.part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * DT_PART;
   for (int e = threadIdx.x; e < DT_PART; e += 256) {
     // element e of the partial row -> (q, slice index)
     int qq, si;
@@ -386,11 +407,13 @@ __global__ __launch_bounds__(256) void dtail_chain_kernel(const float* red, cons
   }
 }
 
-static int dt_grid(long long rows) {
-  // 64 rows per workgroup and iteration; about 4 resident workgroups per CU
-  long long g = (rows + 63) / 64;
-  const long long cap = 1024;
-  return (int)(g < cap ? (g > 0 ? g : 1) : cap);
+// grid (gx, B): gx row blocks per item (64·U rows per block and iteration), about 1024 workgroups in all
+// (4 resident per CU); one partial row per workgroup in the backward
+static int dt_gx(int B, int T) {
+  const int per_item = (T + 127) / 128;
+  int gx = 1024 / B;
+  if (gx > per_item) gx = per_item;
+  return gx > 0 ? gx : 1;
 }
 
 }  // namespace vqa
@@ -407,8 +430,8 @@ extern "C" size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype) {
   (void)C;
   (void)Cu;
   (void)dtype;
-  const int g = dt_grid((long long)B * T);
-  return ((size_t)DT_COMP + (size_t)DT_PART + (size_t)g * DT_PART) * sizeof(float);
+  const size_t g = (size_t)dt_gx(B, T) * B;
+  return ((size_t)DT_COMP + (size_t)DT_PART + g * DT_PART) * sizeof(float);
 }
 
 extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up, const float* w_out,
@@ -424,9 +447,9 @@ extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
   DtArgs a{h, nullptr, y, nullptr, comp, nullptr, B, T};
-  const int g = dt_grid((long long)B * T);
-  if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_fwd_kernel<bf16>, dim3(g), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(dtail_fwd_kernel<float>, dim3(g), dim3(256), 0, s, a);
+  const dim3 g(dt_gx(B, T), B);
+  if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_fwd_kernel<bf16>, g, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dtail_fwd_kernel<float>, g, dim3(256), 0, s, a);
   VQA_LAUNCHED("dtail_fwd_kernel");
   return VQA_OK;
 }
@@ -446,12 +469,12 @@ extern "C" int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, 
   hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
-  const int g = dt_grid((long long)B * T);
+  const dim3 g(dt_gx(B, T), B);
   DtArgs a{h, dy, nullptr, dh, comp, part, B, T};
-  if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_bwd_kernel<bf16>, dim3(g), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(dtail_bwd_kernel<float>, dim3(g), dim3(256), 0, s, a);
+  if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_bwd_kernel<bf16>, g, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dtail_bwd_kernel<float>, g, dim3(256), 0, s, a);
   VQA_LAUNCHED("dtail_bwd_kernel");
-  const vqa_partials_desc d{part, red, nullptr, g, DT_PART, DT_PART, 0};
+  const vqa_partials_desc d{part, red, nullptr, (int)(g.x * g.y), DT_PART, DT_PART, 0};
   if (int rc = vqa_reduce_partials(&d, 1, stream)) return rc;
   const int nbo = (3 * Cu + 3) / 4, nbu = (4 * Cu * DT_C + Cu + 1 + 255) / 256;
   hipLaunchKernelGGL(dtail_chain_kernel, dim3(nbo + nbu), dim3(256), 0, s, red, w_up, b_up, w_out, Cu, nbo, dw_up,

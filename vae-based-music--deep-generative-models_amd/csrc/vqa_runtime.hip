@@ -35,6 +35,41 @@ __global__ __launch_bounds__(256) void mse_kernel(const float* x, const float* r
   if (threadIdx.x == 0) ws[blockIdx.x] = s;
 }
 
+// float4 form (n % 4 == 0, 16-byte aligned buffers): two float4 of every buffer per thread and trip, both
+// loaded before either is used (the second clamped to a valid index, its terms dropped past the end)
+__global__ __launch_bounds__(256) void mse4_kernel(const float* x, const float* r, const float* extra, float* dr,
+                                                  long long n4, float gscale, float* ws) {
+  __shared__ float red[4];
+  float part = 0.f;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += 2 * stride) {
+    const long long j = i + stride < n4 ? i + stride : i;
+    const f32x4 r0 = ((const f32x4*)r)[i], x0 = ((const f32x4*)x)[i];
+    const f32x4 r1 = ((const f32x4*)r)[j], x1 = ((const f32x4*)x)[j];
+    f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0;
+    if (extra) {
+      e0 = ((const f32x4*)extra)[i];
+      e1 = ((const f32x4*)extra)[j];
+    }
+    const f32x4 d0 = r0 - x0, d1 = r1 - x1;
+    f32x4 g0 = gscale * d0, g1 = gscale * d1;
+    if (extra) {
+      g0 = g0 + e0;
+      g1 = g1 + e1;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part += d0[k] * d0[k];
+    ((f32x4*)dr)[i] = g0;
+    if (j != i) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part += d1[k] * d1[k];
+      ((f32x4*)dr)[j] = g1;
+    }
+  }
+  const float s = block_sum_256(part, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
 __global__ __launch_bounds__(256) void mse_reduce_kernel(const float* ws, int n, float scale, float* out) {
   __shared__ float red[4];
   float s = 0.f;
@@ -172,9 +207,15 @@ extern "C" int vqa_mse_loss(const float* x, const float* r, const float* extra_g
   hipStream_t s = (hipStream_t)stream;
   const float inv_n = (float)(1.0 / (double)n);
   const float gscale = (float)(2.0 / (double)n);
-  hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(256), 0, s, x, r, extra_grad, dr, (long long)n, gscale,
-                     (float*)workspace);
-  VQA_LAUNCHED("mse_kernel");
+  if (n % 4 == 0 && ((uintptr_t)x | (uintptr_t)r | (uintptr_t)extra_grad | (uintptr_t)dr) % 16 == 0) {
+    hipLaunchKernelGGL(mse4_kernel, dim3(nb), dim3(256), 0, s, x, r, extra_grad, dr, (long long)(n / 4), gscale,
+                       (float*)workspace);
+    VQA_LAUNCHED("mse4_kernel");
+  } else {
+    hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(256), 0, s, x, r, extra_grad, dr, (long long)n, gscale,
+                       (float*)workspace);
+    VQA_LAUNCHED("mse_kernel");
+  }
   hipLaunchKernelGGL(mse_reduce_kernel, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, inv_n, loss_out);
   VQA_LAUNCHED("mse_reduce_kernel");
   return VQA_OK;

@@ -657,6 +657,63 @@ __global__ __launch_bounds__(256) void spec_gather_kernel(SpecGatherArgs a) {
   }
 }
 
+// The same overlap-add for the usual shapes (<= 4 resolutions, <= 8 frames over a sample, T < 2^24): item =
+// blockIdx.y (no 64-bit division per sample), and every frame read of every resolution is issued before the
+// sums (clamped addresses; a frame past the sample's range is loaded and not added), so a thread's 15-odd
+// loads are in flight together instead of one trip-count-dependent loop iteration at a time. Same sums in the
+// same order: bit-identical to spec_gather_kernel.
+constexpr int kGatherMaxRes = 4, kGatherMaxF = 8;
+__global__ __launch_bounds__(256) void spec_gather8_kernel(SpecGatherArgs a) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int b = 0; b < a.B; ++b) {
+      float s = 0.f;
+      for (int r = 0; r < a.nres; ++r) s += a.lossbr[b * a.nres + r];
+      s = s / (float)a.nres;
+      if (a.item_loss) a.item_loss[b] = s;
+      tot += s;
+    }
+    a.loss_out[0] = tot / (float)a.B;
+  }
+  const int b = blockIdx.y;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < a.T; t += gridDim.x * 256) {
+    float v[kGatherMaxRes][kGatherMaxF];
+    int nf[kGatherMaxRes];
+#pragma unroll
+    for (int r = 0; r < kGatherMaxRes; ++r) {
+      if (r >= a.nres) break;  // uniform
+      const int hop = a.hop[r], win = a.win[r], F = a.F[r];
+      const int f_hi = min(F - 1, t / hop);
+      const int f_lo = t >= win ? (t - win) / hop + 1 : 0;
+      nf[r] = f_hi - f_lo + 1;
+      const float* g = a.fg[r] + (size_t)b * F * win;
+#pragma unroll
+      for (int j = 0; j < kGatherMaxF; ++j) {
+        const int f = min(f_lo + j, f_hi);
+        v[r][j] = g[(size_t)f * win + min(t - f * hop, win - 1)];
+      }
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < kGatherMaxRes; ++r) {
+      if (r >= a.nres) break;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < kGatherMaxF; ++j)
+        if (j < nf[r]) s += v[r][j];
+      acc += a.scale[b * a.nres + r] * s;
+    }
+    a.dr[(size_t)b * a.T + t] = acc;
+  }
+}
+
+static bool spec_gather8_ok(const SpecGatherArgs& a) {
+  if (!a.dr || a.nres > kGatherMaxRes || a.T >= (1 << 24)) return false;
+  for (int r = 0; r < a.nres; ++r)
+    if ((a.win[r] + a.hop[r] - 1) / a.hop[r] > kGatherMaxF) return false;
+  return true;
+}
+
 template <int N>
 static int launch_frames(const SpecFrameArgs& fa, hipStream_t s) {
   constexpr int FPI = 256 / spec_tpf<N>();
@@ -824,6 +881,13 @@ static int spec_loss(const float* tg, const float* r, float* loss_out, float* dr
   ga.B = B;
   ga.T = T;
   ga.nres = nres;
+  if (spec_gather8_ok(ga)) {
+    int nx = (T + 255) / 256;
+    if (nx > 1024) nx = 1024;
+    hipLaunchKernelGGL(spec_gather8_kernel, dim3(nx, B), dim3(256), 0, s, ga);
+    VQA_LAUNCHED("spec_gather8_kernel");
+    return VQA_OK;
+  }
   long long nb = grad ? ((long long)B * T + 255) / 256 : 1;
   if (nb > 8192) nb = 8192;
   hipLaunchKernelGGL(spec_gather_kernel, dim3((int)nb), dim3(256), 0, s, ga);
