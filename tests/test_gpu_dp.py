@@ -104,6 +104,7 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
     Adam step each weight moved by lr * g / (|g| + eps), a ratio anywhere in [-1, 1] where g is rounding noise, so
     the weights are held to two updates per element (|delta w| <= 2 lr) and relative L2 1e-4."""
     lr = 1e-3  # Keras Adam default (vqa_optim.Adam)
+    adam_noise = 1e-3  # Adam moments after the second update, relative L2, outside config 1 (see below)
     nst = 2 * K * D + K  # one level's stats region: m_sumT, n_sum, RT
     rep, bad = [], []
 
@@ -147,6 +148,10 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
             same = n_sum == ss[K * D:K * D + K]
             e = _l2(m_sum.view(K, D)[same], ss[:K * D].view(K, D)[same])
             exact = 1e-6 if world <= 2 else 1e-5  # more rank partial sums, more grouping rounding (measured 4.4e-6 at 4)
+            if phase == "forward" and not strict:
+                # the forward runs on weights two Adam updates apart (see `adam_noise` below): z itself differs by
+                # ~1e-5 (measured 1.2e-5 on the 3-level form, the same in every run)
+                exact = 1e-4
             tol = exact if moved == 0 and not bf16 else (2e-2 if bf16 else 1e-3)
             check(e < tol, f"level {l}: EMA sums of the {int(same.sum())} codes with unchanged counts, L2 {e:.2e}")
     if phase == "step1":
@@ -190,8 +195,13 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
             e = _rel(r0["weights"], s["weights"])
             check(e < 1e-5, f"weights rel {e:.2e} < 1e-5 (max-norm)")
         if phase != "forward":
+            # step 2's gradient is taken at weights whose pure-noise elements moved by up to +-lr in either run (the
+            # step-1 gradients differ in their summation grouping): on the 3-level form that shifts the large
+            # gradients by ~1e-4 — measured 8.6e-5 (2 ranks) and 2.9e-4 (4 ranks), identical in every run, with the
+            # ranks taking turns on the GPU; config 1's architecture stays at 1e-5
             e = max(_l2(r0["adam_m"], s["adam_m"]), _l2(r0["adam_v"], s["adam_v"]))
-            check(e < 1e-5, f"Adam moments relative L2 {e:.2e} < 1e-5")
+            mtol = 1e-5 if strict else adam_noise
+            check(e < mtol, f"Adam moments relative L2 {e:.2e} < {mtol:g}")
     else:
         dw = float((r0["weights"] - s["weights"]).abs().max())
         check(dw <= 2 * lr * 1.01, f"max |delta w| {dw:.2e} <= two Adam updates ({2 * lr:g})")
@@ -203,6 +213,8 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
             check(torch.equal(a["N_t"], b["N_t"]), f"level {l}: N_t bitwise")
             e = max(_rel(a["embeddings"], b["embeddings"]), _rel(a["m_t"], b["m_t"]))
             ctol = 1e-5 * (5 if world > 2 else 1)
+            if phase == "forward" and not strict:
+                ctol = 1e-4  # the forward's EMA on z from weights two Adam updates apart (measured 1.6e-5)
             check(e < ctol, f"level {l}: codebook / m_t rel {e:.2e} < {ctol:g}")
         else:
             e = max(_l2(a["m_t"], b["m_t"]), _l2(a["N_t"], b["N_t"]))

@@ -393,17 +393,7 @@ template <class T> constexpr int rs_fwd_waves() { return sizeof(T) == 2 ? 3 : 2;
 constexpr int rs_fwd_rt(int dt) { return dt > 0 ? 176 : RTM; }
 // (192-row tiles for d <= 9 and 160 for d = 27 — fewer recomputed halo rows per output row — measured slower
 // on the step: 7.59 / 7.53 vs 7.51 ms)
-#ifdef VQA_RS_OCC3
-// A/B variant: 128-row backward tiles for d <= 9 (52.9 KB of LDS: three workgroups per CU) at 3 waves per SIMD
-// (<= 168 VGPRs; the compiler spills the rest to scratch)
-constexpr int rs_bwd_rt(int dt) { return RTM; }
-constexpr int rs_bwd_waves(int dt) { return (dt > 0 && dt <= 9) ? 3 : 2; }
-constexpr int rs_bwd_per_cu(int d) { return (d == 1 || d == 3 || d == 9) ? 3 : 2; }
-#else
 constexpr int rs_bwd_rt(int dt) { return (dt > 0 && dt <= 9) ? 160 : RTM; }
-constexpr int rs_bwd_waves(int dt) { return 2; }
-constexpr int rs_bwd_per_cu(int d) { return 2; }
-#endif
 
 template <class T, int DT, int RT = rs_fwd_rt(DT)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_fwd_waves<T>(), 8)))
@@ -534,8 +524,7 @@ void resblock_fwd_kernel(ResArgs a) {
 // Barriers per tile: H ready, D ready, every read done (then the next tile's staged rows are stored), the
 // stored rows visible: four (the one-buffer form needs five).
 template <class T, int DT, int RT = rs_bwd_rt(DT)>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_bwd_waves(DT), 8)))
-void resblock_bwd_kernel(ResArgs a) {
+__global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
   constexpr int NW = 4;
   constexpr int XS = rs_stride<T>(), NT = RT / 16;
@@ -882,7 +871,7 @@ extern "C" size_t vqa_resblock_bwd_workspace(int B, int T, int C, int dilation, 
   (void)T;
   (void)dilation;
   (void)dtype;
-  return (size_t)2 * rs_cus() * std::max(kResPerCU, rs_bwd_per_cu(1)) * (3 * C * C + C) * sizeof(float);
+  return (size_t)2 * rs_cus() * kResPerCU * (3 * C * C + C) * sizeof(float);
 }
 
 extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, const float* ba, const float* wb,
@@ -900,7 +889,7 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   ResArgs a{x, dy, dx, nullptr, wa, ba, wb, nullptr, (float*)workspace, nullptr, B, T, dilation, 0, 0, 0, 0, 0};
   // at least kResMinTiles tiles per workgroup: a workgroup's weight-gradient partial row (2 x 3,104 fp32) is
   // larger than a tile's activations, so short launches use fewer, longer-lived workgroups
-  plan(a, std::max(kResPerCU, rs_bwd_per_cu(dilation)), bwd_rt_of(dilation), kResMinTiles);
+  plan(a, kResPerCU, bwd_rt_of(dilation), kResMinTiles);
   const int nwg = a.nwg;
   a.part_b = a.part_a + (size_t)nwg * E;
   const int esz = dtype == VQA_BF16 ? 2 : 4;
