@@ -441,6 +441,7 @@ extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up
   VQA_REQUIRE(vqa_dtail_supported(C, Cu, 4, 2, 3, 1, dtype), VQA_E_UNSUPPORTED, "dtail_fwd: unsupported C=%d Cu=%d",
               C, Cu);
   VQA_ARG(workspace && ws_bytes >= vqa_dtail_workspace(B, T, C, Cu, dtype), "dtail_fwd: workspace too small");
+  VQA_ARG(B <= 65535, "dtail_fwd: B=%d items exceed the grid's item rows (65535)", B);
   const hipStream_t s = (hipStream_t)stream;
   float* comp = (float*)workspace;
   hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
@@ -462,6 +463,7 @@ extern "C" int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, 
   VQA_REQUIRE(vqa_dtail_supported(C, Cu, 4, 2, 3, 1, dtype), VQA_E_UNSUPPORTED, "dtail_bwd: unsupported C=%d Cu=%d",
               C, Cu);
   VQA_ARG(workspace && ws_bytes >= vqa_dtail_workspace(B, T, C, Cu, dtype), "dtail_bwd: workspace too small");
+  VQA_ARG(B <= 65535, "dtail_bwd: B=%d items exceed the grid's item rows (65535)", B);
   const hipStream_t s = (hipStream_t)stream;
   float* comp = (float*)workspace;
   float* red = comp + DT_COMP;

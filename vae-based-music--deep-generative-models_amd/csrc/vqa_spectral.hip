@@ -708,7 +708,7 @@ __global__ __launch_bounds__(256) void spec_gather8_kernel(SpecGatherArgs a) {
 }
 
 static bool spec_gather8_ok(const SpecGatherArgs& a) {
-  if (!a.dr || a.nres > kGatherMaxRes || a.T >= (1 << 24)) return false;
+  if (!a.dr || a.nres > kGatherMaxRes || a.T >= (1 << 24) || a.B > 65535) return false;  // items = grid rows
   for (int r = 0; r < a.nres; ++r)
     if ((a.win[r] + a.hop[r] - 1) / a.hop[r] > kGatherMaxF) return false;
   return true;
