@@ -1,6 +1,6 @@
 """Time vqa_vq_argmin_split (bf16 z, exact 3-plane codebook) at the cfg2 levels' row counts (GPU dev tool).
 
-    python tools/argmin_time.py
+    python tools/argmin_time.py [N ...]
 """
 import os
 import sys
@@ -20,7 +20,7 @@ esq = torch.empty(K, device=dev)
 V.vq_sqnorm(E, esq)
 E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=dev)
 V.vq_split_bf16x3(E, E3)
-for N in (262144, 131072, 65536, 32768, 8192):
+for N in [int(a) for a in sys.argv[1:]] or (262144, 131072, 65536, 32768, 8192):
     z = torch.randn(N, D, device=dev, generator=g).to(torch.bfloat16)
     idx = torch.empty(N, dtype=torch.int64, device=dev)
     f = lambda: V.vq_argmin_split(z, E3, esq, idx)  # noqa: E731
