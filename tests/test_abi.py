@@ -71,3 +71,21 @@ def test_reset_rows_tile_semantics():
     # N >= K: K distinct rows
     rows = reset_perm.reset_rows(3, 0, 0, 5000, 2048)
     assert len(np.unique(rows)) == 2048
+
+
+def test_decoder_tail_rejects_more_items_than_grid_rows():
+    """vqa_dtail_fwd / _bwd run one grid row per item (grid.y = B <= 65535): a larger batch is refused with
+    VQA_E_INVALID_ARG before anything is launched (argument checks only: fake device pointers, no GPU needed)."""
+    import ctypes
+    lib = V.lib()
+    combos = [(C, Cu, dt) for C in (32, 64) for Cu in (32, 64) for dt in (V.BF16, V.F32)
+              if lib.vqa_dtail_supported(C, Cu, 4, 2, 3, 1, dt)]
+    assert combos
+    C, Cu, dt = combos[0]
+    B, T = 70000, 8
+    ws = lib.vqa_dtail_workspace(B, T, C, Cu, dt)
+    p = ctypes.c_void_p(0x1000)
+    rc = lib.vqa_dtail_fwd(p, p, p, p, p, p, B, T, C, Cu, dt, p, ws, None)
+    assert rc == -1 and "65535" in V.last_error()
+    rc = lib.vqa_dtail_bwd(p, p, p, p, p, p, p, p, p, p, p, B, T, C, Cu, dt, p, ws, None)
+    assert rc == -1 and "65535" in V.last_error()
