@@ -181,16 +181,16 @@ def prior_legs(a, dev, world, rank):
     pr.capture_train_step(codes, warmup=1)
     pr.train_step(codes)  # the first replay uploads the graph
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.prior_steps):
         pr.train_step(codes)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
@@ -243,11 +243,17 @@ def main():
         local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # VQA_DP_FORCE=1 (rehearsal, tests/test_gpu_rccl.py): the DP branch — process group, the exchange's collective
+    # on the device bucket, split graphs — at N = 1 too (torchrun --nproc-per-node 1), so RCCL runs on one GPU
+    force = os.environ.get("VQA_DP_FORCE") == "1"
+    if world > 1 or force:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        if force:
+            import vqa_dp
+            vqa_dp.FORCE_COLLECTIVE = True
     import vqa_lib as V
     from data_utils import synthetic_batch_device
     from vqvae import VQVAE
@@ -266,16 +272,16 @@ def main():
         for i in range(a.warmup):
             model.train_step(batches[i % 4])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(a.steps):
         model.train_step(batches[i % 4])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
@@ -355,7 +361,7 @@ def main():
                           "graph": not a.no_graph, "final_loss": round(loss, 5)},
                "roofline": roof, "cpu_baseline": cpu, **legs}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

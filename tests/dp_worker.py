@@ -5,7 +5,9 @@ the global batch — eager, or as the two captured hipGraphs around the eager al
 `vqvaes[0](x, training=True)` forward (the EMA on global statistics), and saves the resulting state.
     python tests/dp_worker.py MODE OUT [CONFIG [DTYPE]]   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set)
 CONFIG "cfg1" is BASELINE config 1's architecture; "cfg2_short" is the benched architecture (config 2/3: 3
-levels, K = 2048, down_depth [3,2,2], concurrent level streams) on an 8192-frame chunk.
+levels, K = 2048, down_depth [3,2,2]) on an 8192-frame chunk. The ranks run at the same time on the one GPU; the
+tests start them with VQA_LEVEL_STREAMS=0 (each rank's levels on one stream; DESIGN.md §5: two processes on one
+GPU, one of them with several queues active, corrupt single kernels on this platform).
 """
 import os
 import sys
@@ -48,50 +50,6 @@ def build(B, process_group=None, config="cfg1", dtype="fp32"):
 def batches(world, config="cfg1"):
     from oracle import vqvae_ref as R
     return [R.synthetic_batch(B_LOCAL * world, CONFIGS[config]["input_len"], seed=90 + i) for i in range(3)]
-
-
-def take_turns(m, rank, world):
-    """Run the ranks' GPU work one rank at a time (VQA_DP_TURNS=1, the tests' default): every phase between two
-    collectives — the step's compute, the update after the exchange, the forward-only call's encoder / VQ / EMA /
-    decoder — executes on one rank while the others wait at a gloo barrier. The ranks of these tests share ONE
-    GPU; with two processes' kernels on it at once, results of single kernels were seen to change between
-    otherwise identical runs (wrong values in 16-lane groups, never with one process on the GPU),
-    which the bitwise checks would report as DP errors. Production DP has one process per GPU."""
-    state = {"in": False}
-
-    def turns(fn):
-        def wrapped(*a, **k):
-            if state["in"] or torch.cuda.is_current_stream_capturing():
-                return fn(*a, **k)
-            out = None
-            for r in range(world):
-                if r == rank:
-                    state["in"] = True
-                    try:
-                        out = fn(*a, **k)
-                        torch.cuda.synchronize()
-                    finally:
-                        state["in"] = False
-                dist.barrier()
-            return out
-        return wrapped
-
-    m._compute = turns(m._compute)
-    m._update = turns(m._update)
-
-    def replay():
-        g1, g2 = m._graph
-        turns(g1.replay)()
-        if g2 is not None:
-            m._exchange()
-            turns(g2.replay)()
-
-    m._replay = replay
-    for l in range(m.levels):
-        m.encoders[l].forward = turns(m.encoders[l].forward)
-        m.decoders[l].forward = turns(m.decoders[l].forward)
-        m.vqs[l].forward = turns(m.vqs[l].forward)
-        m.vqs[l].apply_ema = turns(m.vqs[l].apply_ema)
 
 
 def snapshot(m):
@@ -141,8 +99,6 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = build(B_LOCAL, config=config, dtype=dtype)
-    if os.environ.get("VQA_DP_TURNS", "1") == "1":
-        take_turns(m, rank, world)
     xs = [x[rank * B_LOCAL:(rank + 1) * B_LOCAL] for x in batches(world, config)]
     local, post = [], []
     if os.environ.get("VQA_DP_PROBE") == "1":

@@ -55,9 +55,12 @@ def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False, batch=2, pha
     procs, outs = [], []
     for r in range(world):
         out = str(tmp_path / f"{mode}_{config}_{dtype}_rank{r}.pt")
+        # the ranks share the one test GPU and run at the same time, each with its levels on one stream: two
+        # processes on one GPU while one of them has several queues active get single kernels' results corrupted on
+        # this platform (tools/cotenant.py); the product's DP has one process per GPU
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), VQA_DP_PROBE="1" if probe else "0", VQA_DP_BATCH=str(batch),
-                   VQA_DP_PHASES=phases)
+                   VQA_DP_PHASES=phases, VQA_LEVEL_STREAMS="0")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out, config, dtype],
                                       env=env))
         outs.append(out)
@@ -104,7 +107,9 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
     Adam step each weight moved by lr * g / (|g| + eps), a ratio anywhere in [-1, 1] where g is rounding noise, so
     the weights are held to two updates per element (|delta w| <= 2 lr) and relative L2 1e-4."""
     lr = 1e-3  # Keras Adam default (vqa_optim.Adam)
-    adam_noise = 1e-3  # Adam moments after the second update, relative L2, outside config 1 (see below)
+    # Adam moments after the second update, relative L2, outside config 1: ~2x the drift measured (8.6e-5 at 2
+    # ranks, 2.9e-4 at 4 ranks; deterministic per run, see below)
+    adam_noise = 2e-4 if world <= 2 else 6e-4
     nst = 2 * K * D + K  # one level's stats region: m_sumT, n_sum, RT
     rep, bad = [], []
 
@@ -151,7 +156,7 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
             if phase == "forward" and not strict:
                 # the forward runs on weights two Adam updates apart (see `adam_noise` below): z itself differs by
                 # ~1e-5 (measured 1.2e-5 on the 3-level form, the same in every run)
-                exact = 1e-4
+                exact = 3e-5 if world <= 2 else 1e-4
             tol = exact if moved == 0 and not bf16 else (2e-2 if bf16 else 1e-3)
             check(e < tol, f"level {l}: EMA sums of the {int(same.sum())} codes with unchanged counts, L2 {e:.2e}")
     if phase == "step1":
@@ -197,8 +202,8 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
         if phase != "forward":
             # step 2's gradient is taken at weights whose pure-noise elements moved by up to +-lr in either run (the
             # step-1 gradients differ in their summation grouping): on the 3-level form that shifts the large
-            # gradients by ~1e-4 — measured 8.6e-5 (2 ranks) and 2.9e-4 (4 ranks), identical in every run, with the
-            # ranks taking turns on the GPU; config 1's architecture stays at 1e-5
+            # gradients by ~1e-4 — measured 8.6e-5 (2 ranks) and 2.9e-4 (4 ranks), identical in every run; config 1's
+            # architecture stays at 1e-5
             e = max(_l2(r0["adam_m"], s["adam_m"]), _l2(r0["adam_v"], s["adam_v"]))
             mtol = 1e-5 if strict else adam_noise
             check(e < mtol, f"Adam moments relative L2 {e:.2e} < {mtol:g}")
@@ -214,7 +219,7 @@ def _compare(r0, r1, s, K, D, L, phase, bf16, strict=False, world=2, full_size=F
             e = max(_rel(a["embeddings"], b["embeddings"]), _rel(a["m_t"], b["m_t"]))
             ctol = 1e-5 * (5 if world > 2 else 1)
             if phase == "forward" and not strict:
-                ctol = 1e-4  # the forward's EMA on z from weights two Adam updates apart (measured 1.6e-5)
+                ctol = 4e-5 if world <= 2 else 1e-4  # the forward's EMA on z from weights two Adam updates apart (measured 1.6e-5)
             check(e < ctol, f"level {l}: codebook / m_t rel {e:.2e} < {ctol:g}")
         else:
             e = max(_l2(a["m_t"], b["m_t"]), _l2(a["N_t"], b["N_t"]))

@@ -366,15 +366,20 @@ def test_argmin_nonfinite_rows_index_zero(cuda, path):
     esq = torch.empty(K, device=cuda)
     V.vq_sqnorm(Ed, esq)
     idx = torch.empty(N, dtype=torch.int64, device=cuda)
+    mind = torch.empty(N, device=cuda)
     if path == "bf16_split":
         E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=cuda)
         V.vq_split_bf16x3(Ed, E3)
-        V.vq_argmin_split(zd, E3, esq, idx)  # N small: the codebook is split across workgroups
+        V.vq_argmin_split(zd, E3, esq, idx, mind)  # N small: the codebook is split across workgroups
     else:
-        V.vq_argmin(zd, Ed, esq, idx)
+        V.vq_argmin(zd, Ed, esq, idx, mind)
     got = idx.cpu()
     assert int(got[5]) == 0 and int(got[17]) == 0 and int(got[18]) == 0
     assert bool(((got >= 0) & (got < K)).all())
+    # the reported min distance of such a row is +inf (the distance form's value: no finite distance exists)
+    md = mind.cpu()
+    assert all(float(md[i]) == float("inf") for i in (5, 17, 18)), md[[5, 17, 18]]
+    assert bool(torch.isfinite(md[[i for i in range(N) if i not in (5, 17, 18)]]).all())
     q = torch.empty_like(zd)
     commit = torch.zeros(1, device=cuda)
     m_sumT = torch.zeros(K, D, device=cuda)
@@ -382,3 +387,58 @@ def test_argmin_nonfinite_rows_index_zero(cuda, path):
     V.vq_quantize(zd, Ed.t().contiguous(), idx, q, commit, m_sumT, n_sum, 0.25)
     torch.cuda.synchronize()
     assert float(n_sum.sum()) == N
+
+
+def test_argmin_split_near_ties_at_large_norm(cuda):
+    """Documented divergence from the reference's formula (VectorQuantizer.py:173-185 computes the fp32 distance
+    (|z|^2 + |e|^2) - 2 z.e): the split kernel maximises key = z.e - |e|^2 / 2, which carries no |z|^2 term. Rows
+    built with a large |z| (|z|^2 ~ 2.6e5) and two codes whose exact distances differ by far less than the fp32
+    rounding of |z|^2: the fp32 distance form (a numpy restatement of the reference's op order) picks the other
+    code on some of them, while the kernel picks the EXACT (fp64) nearest code on every row whose exact margin
+    exceeds the key form's own rounding (z.e accumulated in fp32 over exact bf16 plane products)."""
+    D, K, N = 64, 256, 4096
+    g = torch.Generator().manual_seed(11)
+    E = (torch.rand(D, K, generator=g) - 0.5) * 0.1
+    z = (torch.randn(N, D, generator=g) * 64.0).to(torch.bfloat16)  # |z|^2 ~ 2.6e5
+    zf = z.double()
+    # on every 16th row a second code is moved to 4e-3 (exact distance) behind the row's nearest code: far below the
+    # fp32 rounding of |z|^2 (ulp 0.03) that the distance form carries, far above the key form's rounding
+    Ed = E.double()
+    d = (zf * zf).sum(1, keepdim=True) + (Ed * Ed).sum(0) - 2 * zf @ Ed
+    best = d.argmin(1)
+    for r in range(0, N, 16):  # one crafted pair per 16 rows (the codes are shared by the rows)
+        b = int(best[r])
+        c = (b + 1 + r // 16) % K
+        # e_c = e_b + t * u with u orthogonal to (z_r - e_b): |z_r - e_c|^2 = |z_r - e_b|^2 + t^2 |u|^2
+        v = zf[r] - Ed[:, b]
+        u = torch.randn(D, generator=g, dtype=torch.float64)
+        u -= (u @ v) / (v @ v) * v
+        u /= u.norm()
+        Ed[:, c] = Ed[:, b] + 0.004 ** 0.5 * u  # exact margin 4e-3 on row r
+    E = Ed.float()
+    Ed = E.double()
+    d = (zf * zf).sum(1, keepdim=True) + (Ed * Ed).sum(0) - 2 * zf @ Ed
+    exact = d.argmin(1)
+    top2 = torch.topk(d, 2, dim=1, largest=False).values
+    margin = top2[:, 1] - top2[:, 0]
+    # the reference's fp32 op order: (|z|^2 + |e|^2) - 2 z.e, each term rounded to fp32
+    z32, E32 = z.float().numpy(), E.numpy()
+    zz = (z32 * z32).sum(1, keepdims=True, dtype=np.float32)
+    ee = (E32 * E32).sum(0, keepdims=True, dtype=np.float32)
+    ref32 = torch.from_numpy(np.argmin((zz + ee) - np.float32(2.0) * (z32 @ E32), axis=1))
+    Ec, zc = E.to(cuda), z.to(cuda)
+    esq = torch.empty(K, device=cuda)
+    V.vq_sqnorm(Ec, esq)
+    E3 = torch.empty(K, 3, D, dtype=torch.bfloat16, device=cuda)
+    V.vq_split_bf16x3(Ec, E3)
+    idx = torch.empty(N, dtype=torch.int64, device=cuda)
+    V.vq_argmin_split(zc, E3, esq, idx)
+    got = idx.cpu()
+    # key-form rounding: z.e of a few tens, fp32 accumulation over 3 x 64 exact products -> ~1e-4 absolute
+    clear = margin > 3e-3
+    assert clear.float().mean() > 0.9
+    assert torch.equal(got[clear], exact[clear]), f"{int((got[clear] != exact[clear]).sum())} clear rows differ"
+    diverge = int((ref32 != exact).sum())
+    print(f"rows where the fp32 distance form misses the exact nearest code: {diverge} of {N}; "
+          f"kernel misses on clear rows: 0; near-tie rows (margin <= 3e-3): {int((~clear).sum())}")
+    assert diverge > 0, "the construction should defeat the fp32 distance form on some rows"

@@ -1,9 +1,9 @@
 #!/bin/bash
-# One GPU call of round 4: steps given as "name:command" words; each runs under its own time limit. A step that
+# One GPU call: steps given as "name:command" words; each runs under its own time limit. A step that
 # fails its assertions (exit 1) lets the next one run; a time limit, abort or fault (any other non-zero status)
 # ends the script there.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=gpurun_out/${TAG:-r4}
+OUT=gpurun_out/${TAG:-call}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 LIMIT=${LIMIT:-600}

@@ -132,6 +132,14 @@ struct DtArgs {
   int B, T;
 };
 
+// the value of lane ^ 1 / lane ^ 2 by a DPP quad permute (VALU, no LDS crossbar)
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+}
+
 // y[n, 2j + p] for 16 rows per wave and iteration; grid (row blocks, items), grid-stride over the item's rows
 template <class T>
 __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
@@ -182,10 +190,17 @@ __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
       }
       if (j == 0) y0 -= c0;        // out conv padding at t = 0 drops tap k = 0
       if (j == a.T - 1) y1 -= c1;  // ... and at t = 2T - 1 tap k = 2
+#ifdef VQA_DT_DPP
+      y0 += quad_xor1(y0);
+      y1 += quad_xor1(y1);
+      y0 += quad_xor2(y0);
+      y1 += quad_xor2(y1);
+#else
       y0 += __shfl_xor(y0, 1, 64);
       y1 += __shfl_xor(y1, 1, 64);
       y0 += __shfl_xor(y0, 2, 64);
       y1 += __shfl_xor(y1, 2, 64);
+#endif
       if (j < a.T && q == 0) {
         y0 += bias - (j == 0 ? b0 : 0.f);
         y1 += bias - (j == a.T - 1 ? b2 : 0.f);
@@ -407,10 +422,11 @@ __global__ __launch_bounds__(256) void dtail_chain_kernel(const float* red, cons
   }
 }
 
-// grid (gx, B): gx row blocks per item (64·U rows per block and iteration), about 1024 workgroups in all
-// (4 resident per CU); one partial row per workgroup in the backward
-static int dt_gx(int B, int T) {
-  const int per_item = (T + 127) / 128;
+// grid (gx, B): gx row blocks per item (rows_per_block rows per block and iteration: the forward's 4 waves x 16 x
+// U = 3 = 192, the backward's 4 x 16 x U = 2 = 128), about 1024 workgroups in all (4 resident per CU); one partial
+// row per workgroup in the backward
+static int dt_gx(int B, int T, int rows_per_block) {
+  const int per_item = (T + rows_per_block - 1) / rows_per_block;
   int gx = 1024 / B;
   if (gx > per_item) gx = per_item;
   return gx > 0 ? gx : 1;
@@ -430,7 +446,7 @@ extern "C" size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype) {
   (void)C;
   (void)Cu;
   (void)dtype;
-  const size_t g = (size_t)dt_gx(B, T) * B;
+  const size_t g = (size_t)dt_gx(B, T, 128) * B;  // the backward's partial rows
   return ((size_t)DT_COMP + (size_t)DT_PART + g * DT_PART) * sizeof(float);
 }
 
@@ -448,7 +464,7 @@ extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
   DtArgs a{h, nullptr, y, nullptr, comp, nullptr, B, T};
-  const dim3 g(dt_gx(B, T), B);
+  const dim3 g(dt_gx(B, T, 192), B);
   if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_fwd_kernel<bf16>, g, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dtail_fwd_kernel<float>, g, dim3(256), 0, s, a);
   VQA_LAUNCHED("dtail_fwd_kernel");
@@ -471,7 +487,7 @@ extern "C" int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, 
   hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
-  const dim3 g(dt_gx(B, T), B);
+  const dim3 g(dt_gx(B, T, 128), B);
   DtArgs a{h, dy, nullptr, dh, comp, part, B, T};
   if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_bwd_kernel<bf16>, g, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dtail_bwd_kernel<float>, g, dim3(256), 0, s, a);

@@ -314,10 +314,11 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
       const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
       if ((lane & 15) == 0 && row < N) {
         // |z|^2 - 2 key (+inf for a row with no finite key). A row with a non-finite |z|^2 has no finite distance
-        // to any code (inf - inf or NaN): code 0 of the span, as the distance form resolves it
+        // to any code (inf - inf or NaN): code 0 of the span, as the distance form resolves it, and min distance
+        // +inf, as the distance form reports it (a NaN would also break the packed keys' order in the merge)
         const float zr = zq[rt][r];
         const bool finite = zr < __builtin_inff();
-        const float dist = finite ? __builtin_fmaf(-2.0f, b, zr) : zr;
+        const float dist = finite ? __builtin_fmaf(-2.0f, b, zr) : __builtin_inff();
         if (!finite) bi = kbeg;
         if (packed) {
           atomicMin((unsigned long long*)idx + row, vq_pack(dist, bi));
@@ -580,9 +581,10 @@ static int quantize_blocks(long long total) {
   return (int)b;
 }
 
-// the vectorised forms apply: D = 32 / 64, 16-byte aligned rows, 32-bit piece indices
+// the vectorised forms apply: D = 32 / 64, 16-byte aligned rows, 32-bit piece indices — including the grid-stride
+// loop's last increment (a piece index plus the largest stride, 4096 blocks x 256, stays below 2^31)
 static bool vq_vec8_ok(long long N, int D, std::initializer_list<const void*> ptrs) {
-  if ((D != 32 && D != 64) || N * (D / 8) >= (1ll << 31)) return false;
+  if ((D != 32 && D != 64) || N * (D / 8) + 4096ll * 256 >= (1ll << 31)) return false;
   for (const void* p : ptrs)
     if ((uintptr_t)p % 16) return false;
   return true;

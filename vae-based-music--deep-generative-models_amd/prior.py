@@ -806,10 +806,10 @@ class Prior:
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool):
             self._compute(c, u, teacher_force_rate, None, l)
-            if self._world() == 1:
+            if not vqa_dp.active(self.process_group):
                 self._apply()
         g2 = None
-        if self._world() > 1:  # two graphs around the eager all_reduce
+        if vqa_dp.active(self.process_group):  # two graphs around the eager all_reduce
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=pool):
                 self._apply()

@@ -16,13 +16,13 @@ from __future__ import annotations
 
 from typing import Dict, Sequence
 
-import os
-
 import torch
 import torch.distributed as dist
 
-# diagnosis only (tools/dp_diag.py, round-3 failure study): hand gloo the device bucket as the RCCL path does
-_GLOO_DEVICE = os.environ.get("VQA_DP_GLOO_DEVICE") == "1"
+# Test hook (tests/test_gpu_rccl.py): take the data-parallel path — the exchange's collective on the device bucket,
+# the EMA after it, two graphs around it — even in a process group of ONE rank, so the RCCL branch runs on a
+# one-GPU box. Off in the product: at world size 1 the step needs no exchange.
+FORCE_COLLECTIVE = False
 
 
 def bucket_layout(n_params: int, stats_sizes: Sequence[int], levels: int, align: int = 64) -> Dict[str, object]:
@@ -50,17 +50,22 @@ def rank(group=None) -> int:
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
+def active(group=None) -> bool:
+    """Does the step take the data-parallel path (exchange, EMA after it, split graphs)?"""
+    return world_size(group) > 1 or (FORCE_COLLECTIVE and dist.is_available() and dist.is_initialized())
+
+
 def exchange(bucket: torch.Tensor, group=None) -> int:
-    """Sum the bucket over ranks (no-op on one rank). Returns the world size (grad scale = 1/W)."""
+    """Sum the bucket over ranks (no-op on one rank). Returns the world size (grad scale = 1/W).
+
+    RCCL over xGMI ("nccl"): one all_reduce on the device bucket, queued on the current (producer) stream — which
+    has joined the levels' streams — so it reads the finished gradients and every later launch on that stream
+    reads the sum. The gloo rehearsal backend (the tests, bench under VQA_DIST_BACKEND=gloo) gets the bucket staged
+    through host memory here: a blocking copy out on the producer stream, the CPU all_reduce, a copy back on the
+    same stream (gloo's own device staging runs on a side stream of its own; host staging keeps this one order)."""
     w = world_size(group)
-    if w > 1:
-        # RCCL over xGMI ("nccl"): ordered on the current stream, on the device bucket. The gloo rehearsal
-        # backend (tests, bench under VQA_DIST_BACKEND=gloo) stages the bucket through host memory itself: a
-        # blocking copy out on the producer stream (which has joined the levels' streams), the CPU all_reduce,
-        # and a copy back on the same stream. Handing gloo the device bucket (its own pinned staging on a pool
-        # stream behind an event) left the 2-rank bf16 graph-warm-up test with a sum that missed part of the
-        # last-produced gradients (level 2, encoder block 0) in a few runs, even after a host sync first.
-        if bucket.is_cuda and dist.get_backend(group) == dist.Backend.GLOO and not _GLOO_DEVICE:
+    if active(group):
+        if bucket.is_cuda and dist.get_backend(group) == dist.Backend.GLOO:
             host = bucket.to("cpu")  # synchronous: waits for the producer stream
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
             bucket.copy_(host)

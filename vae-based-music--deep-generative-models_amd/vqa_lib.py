@@ -13,7 +13,8 @@ from typing import Optional
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvqa.so")
+# VQA_LIB_PATH: another build of the same sources (A/B and diagnosis tools only; the product loads libvqa.so)
+LIB_PATH = os.environ.get("VQA_LIB_PATH") or os.path.join(HERE, "libvqa.so")
 
 F32, BF16 = 0, 1
 PRE_RELU, ADD_RESIDUAL, POST_MASK, X_F32, Y_F32 = 1, 2, 4, 8, 16
@@ -185,7 +186,15 @@ def ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr())
 
 
+# Test hook (tests/test_gpu_race.py, tools/cotenant.py): a callable run right before every libvqa launch is
+# queued, on the launching thread with the launch's stream current — the race tests use it to put random spin
+# delays in front of launches, so every cross-stream ordering the step relies on is exercised. None in the product.
+launch_hook = None
+
+
 def stream():
+    if launch_hook is not None:
+        launch_hook()
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 

@@ -234,7 +234,7 @@ class VQVAE:
         self._stats_region.zero_()
         main = torch.cuda.current_stream(self.device)
         streams = self._level_streams()
-        ema_in_level = self._world() == 1 and not self._r3_layout
+        ema_in_level = not vqa_dp.active(self.process_group) and not self._r3_layout
         if streams is None or self._r3_layout:
             target = SpectralTarget(x)
         if streams is None:
@@ -291,7 +291,7 @@ class VQVAE:
         world = self._world()
         if apply_grads:
             self.optimizer.apply(self.store, grad_scale=1.0 / world)
-        if world > 1 or self._r3_layout:  # on one device the levels' chains applied their EMA already (_compute)
+        if vqa_dp.active(self.process_group) or self._r3_layout:  # else the levels' chains applied it (_compute)
             for vq in self.vqs:
                 vq.apply_ema(update_trackers=False)
         # update_metrics (vqvae.py:262-304) + the VQ trackers: one launch
@@ -388,10 +388,10 @@ class VQVAE:
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=self._graph_pool):
             self._compute(self._graph_x, True)
-            if self._world() == 1:
+            if not vqa_dp.active(self.process_group):
                 self._update(True)
         g2 = None
-        if self._world() > 1:
+        if vqa_dp.active(self.process_group):
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=self._graph_pool):
                 self._update(True)
