@@ -391,25 +391,25 @@ def test_argmin_nonfinite_rows_index_zero(cuda, path):
 
 def test_argmin_split_near_ties_at_large_norm(cuda):
     """Documented divergence from the reference's formula (VectorQuantizer.py:173-185 computes the fp32 distance
-    (|z|^2 + |e|^2) - 2 z.e): the split kernel maximises key = z.e - |e|^2 / 2, which carries no |z|^2 term. Rows
-    built with a large |z| (|z|^2 ~ 2.6e5) and two codes whose exact distances differ by far less than the fp32
-    rounding of |z|^2: the fp32 distance form (a numpy restatement of the reference's op order) picks the other
-    code on some of them, while the kernel picks the EXACT (fp64) nearest code on every row whose exact margin
-    exceeds the key form's own rounding (z.e accumulated in fp32 over exact bf16 plane products)."""
-    D, K, N = 64, 256, 4096
+    (|z|^2 + |e|^2) - 2 z.e and takes its argmin): the split kernel maximises key = z.e - |e|^2 / 2 (no |z|^2 term)
+    on bf16 MFMA over the exact hi/mid/lo planes of E. Rows with a large |z| (|z|^2 ~ 2.6e5) get a second code
+    4e-3 (exact distance) behind their nearest one — a near tie by SURVEY.md §8c's definition (margin below
+    1e-5 |d_min| ~ 2.6), where the build is not required to agree with the fp64 argmin:
+      every row with a margin above the §8c bound takes the exact nearest code (as everywhere else);
+      on the crafted near ties the kernel misses the exact nearest code on no more rows than the reference's own
+      fp32 distance form does (a numpy restatement of its op order): the key form has no
+      |z|^2 rounding (ulp 0.03 at this norm) to lose the margin in."""
+    D, K, N = 64, 1024, 4096
     g = torch.Generator().manual_seed(11)
     E = (torch.rand(D, K, generator=g) - 0.5) * 0.1
     z = (torch.randn(N, D, generator=g) * 64.0).to(torch.bfloat16)  # |z|^2 ~ 2.6e5
     zf = z.double()
-    # on every 16th row a second code is moved to 4e-3 (exact distance) behind the row's nearest code: far below the
-    # fp32 rounding of |z|^2 (ulp 0.03) that the distance form carries, far above the key form's rounding
     Ed = E.double()
     d = (zf * zf).sum(1, keepdim=True) + (Ed * Ed).sum(0) - 2 * zf @ Ed
     best = d.argmin(1)
-    for r in range(0, N, 16):  # one crafted pair per 16 rows (the codes are shared by the rows)
-        b = int(best[r])
-        c = (b + 1 + r // 16) % K
-        # e_c = e_b + t * u with u orthogonal to (z_r - e_b): |z_r - e_c|^2 = |z_r - e_b|^2 + t^2 |u|^2
+    for i, r in enumerate(range(0, N, 32)):  # every 32nd row: its nearest code b gets a twin c (a code of its own)
+        b, c = int(best[r]), K - 1 - i
+        # e_c = e_b + t u with u orthogonal to (z_r - e_b): |z_r - e_c|^2 = |z_r - e_b|^2 + t^2 |u|^2
         v = zf[r] - Ed[:, b]
         u = torch.randn(D, generator=g, dtype=torch.float64)
         u -= (u @ v) / (v @ v) * v
@@ -419,8 +419,6 @@ def test_argmin_split_near_ties_at_large_norm(cuda):
     Ed = E.double()
     d = (zf * zf).sum(1, keepdim=True) + (Ed * Ed).sum(0) - 2 * zf @ Ed
     exact = d.argmin(1)
-    top2 = torch.topk(d, 2, dim=1, largest=False).values
-    margin = top2[:, 1] - top2[:, 0]
     # the reference's fp32 op order: (|z|^2 + |e|^2) - 2 z.e, each term rounded to fp32
     z32, E32 = z.float().numpy(), E.numpy()
     zz = (z32 * z32).sum(1, keepdims=True, dtype=np.float32)
@@ -434,11 +432,16 @@ def test_argmin_split_near_ties_at_large_norm(cuda):
     idx = torch.empty(N, dtype=torch.int64, device=cuda)
     V.vq_argmin_split(zc, E3, esq, idx)
     got = idx.cpu()
-    # key-form rounding: z.e of a few tens, fp32 accumulation over 3 x 64 exact products -> ~1e-4 absolute
-    clear = margin > 3e-3
-    assert clear.float().mean() > 0.9
-    assert torch.equal(got[clear], exact[clear]), f"{int((got[clear] != exact[clear]).sum())} clear rows differ"
-    diverge = int((ref32 != exact).sum())
-    print(f"rows where the fp32 distance form misses the exact nearest code: {diverge} of {N}; "
-          f"kernel misses on clear rows: 0; near-tie rows (margin <= 3e-3): {int((~clear).sum())}")
-    assert diverge > 0, "the construction should defeat the fp32 distance form on some rows"
+    ok = _margin_mask(d)
+    top2 = torch.topk(d, 2, dim=1, largest=False).values
+    # the near ties the construction left (a later crafting may move an earlier pair's code again)
+    rows = torch.nonzero(top2[:, 1] - top2[:, 0] < 1e-2).flatten()  # 93 (a crafted code may be a later row's b)
+    assert len(rows) >= 60 and not ok[rows].any(), "near ties by the §8c bound"
+    assert ok.float().mean() > 0.5  # 68 %: at |z|^2 ~ 2.6e5 the §8c bound (~2.6) is wide against K = 1024 codes
+    assert torch.equal(got[ok], exact[ok]), f"{int((got[ok] != exact[ok]).sum())} rows above the §8c margin differ"
+    miss_kernel = int((got[rows] != exact[rows]).sum())
+    miss_ref32 = int((ref32[rows] != exact[rows]).sum())
+    print(f"crafted near ties (exact margin < 1e-2, |z|^2 ~ 2.6e5): kernel misses the exact nearest code on "
+          f"{miss_kernel} of {len(rows)}, the fp32 distance form on {miss_ref32}")
+    assert miss_ref32 > 0, "the construction should defeat the fp32 distance form on some rows"
+    assert miss_kernel <= miss_ref32, (miss_kernel, miss_ref32)

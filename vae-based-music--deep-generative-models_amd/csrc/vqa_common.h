@@ -44,11 +44,112 @@ template <> __device__ __forceinline__ void st4<bf16>(bf16* p, f32x4 v) {
   *(bf16x4*)p = o;
 }
 
-__device__ __forceinline__ float warp_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- cross-lane moves on the VALU (DPP, v_permlane*_swap, v_readlane) ------------------------------------
+// No kernel of the library uses ds_bpermute_b32 / ds_swizzle (what __shfl* compiles to: the LDS crossbar). On this
+// platform, while kernels of SEVERAL hardware queues share the CUs, ds_bpermute returned wrong data in lanes 48-63
+// of a wave (the decoder tail's row sums) and a spectral kernel's results changed run to run; with these VALU forms
+// both stayed bitwise repeatable (tools/cotenant.py). Every caller below has all 64 lanes active.
+// Partner helpers return the value of one partner lane; each step of a reduction pairs the two halves of the group
+// the previous steps reduced, so a reduction over a 16-lane row is xor1 -> xor2 -> hmirror -> mirror, and the
+// same fp32 sums are formed in both lanes of every pair (a + b = b + a: every lane ends with identical bits).
+namespace xl {
+template <int CTRL> __device__ __forceinline__ int dpp(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+template <int CTRL> __device__ __forceinline__ float dpp(float v) { return __int_as_float(dpp<CTRL>(__float_as_int(v))); }
+template <class T> __device__ __forceinline__ T xor1(T v) { return dpp<0xB1>(v); }      // quad_perm [1,0,3,2]
+template <class T> __device__ __forceinline__ T xor2(T v) { return dpp<0x4E>(v); }      // quad_perm [2,3,0,1]
+template <class T> __device__ __forceinline__ T hmirror(T v) { return dpp<0x141>(v); }  // row_half_mirror: 7 - i
+template <class T> __device__ __forceinline__ T mirror(T v) { return dpp<0x140>(v); }   // row_mirror: 15 - i
+template <class T> __device__ __forceinline__ T ror4(T v) { return dpp<0x124>(v); }     // row_ror:4
+template <class T> __device__ __forceinline__ T ror8(T v) { return dpp<0x128>(v); }     // row_ror:8
+// the values of lanes l and l ^ 16 (resp. l ^ 32), in an order the caller must not rely on (symmetric use only)
+__device__ __forceinline__ void pair16(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void pair32(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void pair16(int v, int& a, int& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  a = (int)r[0];
+  b = (int)r[1];
+}
+__device__ __forceinline__ void pair32(int v, int& a, int& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  a = (int)r[0];
+  b = (int)r[1];
+}
+__device__ __forceinline__ float sum16(float v) { float a, b; pair16(v, a, b); return a + b; }  // v[l] + v[l ^ 16]
+__device__ __forceinline__ float sum32(float v) { float a, b; pair32(v, a, b); return a + b; }  // v[l] + v[l ^ 32]
+__device__ __forceinline__ float max16(float v) { float a, b; pair16(v, a, b); return fmaxf(a, b); }
+__device__ __forceinline__ float max32(float v) { float a, b; pair32(v, a, b); return fmaxf(a, b); }
+// sum over the lane's 16-lane row, in every lane of the row
+__device__ __forceinline__ float row_sum(float v) {
+  v += xor1(v);
+  v += xor2(v);
+  v += hmirror(v);
+  return v + mirror(v);
+}
+__device__ __forceinline__ float row_max(float v) {
+  v = fmaxf(v, xor1(v));
+  v = fmaxf(v, xor2(v));
+  v = fmaxf(v, hmirror(v));
+  return fmaxf(v, mirror(v));
+}
+// sum over the aligned group of R consecutive lanes (R a power of two <= 64), in every lane of the group
+template <int R> __device__ __forceinline__ float grp_sum(float v) {
+  if constexpr (R >= 2) v += xor1(v);
+  if constexpr (R >= 4) v += xor2(v);
+  if constexpr (R >= 8) v += hmirror(v);
+  if constexpr (R >= 16) v += mirror(v);
+  if constexpr (R >= 32) v = sum16(v);
+  if constexpr (R >= 64) v = sum32(v);
   return v;
 }
+// sum over the lanes with equal (lane mod R), R a power of two <= 64 (in lane q the rotations pair q with q + 4,
+// q + 8 inside its row: every lane of a residue class ends with the class sum, the lanes < R with the same
+// association)
+template <int R> __device__ __forceinline__ float grp_combine(float v) {
+  if constexpr (R <= 1) v += xor1(v);
+  if constexpr (R <= 2) v += xor2(v);
+  if constexpr (R <= 4) v += ror4(v);
+  if constexpr (R <= 8) v += ror8(v);
+  if constexpr (R <= 16) v = sum16(v);
+  if constexpr (R <= 32) v = sum32(v);
+  return v;
+}
+// inclusive scan over the wave: Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8; lanes shifted in from
+// outside the row add 0), then the totals of the rows below (lanes 15, 31, 47 by v_readlane)
+template <int CTRL> __device__ __forceinline__ int dpp0(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ int incl_scan(int x) {
+  x += dpp0<0x111>(x);
+  x += dpp0<0x112>(x);
+  x += dpp0<0x114>(x);
+  x += dpp0<0x118>(x);
+  const int t0 = __builtin_amdgcn_readlane(x, 15), t1 = __builtin_amdgcn_readlane(x, 31),
+            t2 = __builtin_amdgcn_readlane(x, 47), row = (threadIdx.x & 63) >> 4;
+  return x + (row > 0 ? t0 : 0) + (row > 1 ? t1 : 0) + (row > 2 ? t2 : 0);
+}
+// value of lane `src` (wave-uniform) in every lane
+__device__ __forceinline__ float bcast(float v, int src) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src)); }
+}  // namespace xl
+
+// Every LDS access the wave has issued has completed (reads returned, writes done): s_waitcnt lgkmcnt(0). A wave
+// that rewrites LDS it has just read (or reads what it has just written) without a workgroup barrier calls this
+// between the two: the same run-to-run changes as above (lanes 48-63) showed with in-place LDS passes that relied on
+// the wave's LDS instructions executing in issue order. (gfx9 s_waitcnt layout: vmcnt [3:0] + [15:14] = 63, expcnt
+// [6:4] = 7 — no wait — and lgkmcnt [11:8] = 0.)
+__device__ __forceinline__ void lds_wave_fence() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// sum over the 64 lanes, in every lane
+__device__ __forceinline__ float warp_sum(float v) { return xl::sum32(xl::sum16(xl::row_sum(v))); }
+__device__ __forceinline__ float warp_max(float v) { return xl::max32(xl::max16(xl::row_max(v))); }
 
 // block (256 threads) sum; result valid in all threads. red must hold >= 4 floats.
 __device__ __forceinline__ float block_sum_256(float v, float* red) {

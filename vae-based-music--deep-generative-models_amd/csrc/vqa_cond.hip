@@ -31,11 +31,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const float* table, cons
 // owns channels lane, lane + 64, ... (C <= 64 * LC); wave reductions in a fixed butterfly order.
 constexpr int kLnMaxLC = 16;  // C <= 1024
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return warp_sum(v); }
 
 template <class T, int LC>
 __device__ __forceinline__ void ln_row_stats(const T* xr, int C, float (&xv)[LC], float& mean, float& inv, float eps) {
@@ -124,11 +120,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* x, const T*
 // Vectorised forms for C = 8R (R = lanes per row, a power of two <= 64): each lane owns 8 consecutive channels
 // (one 16-byte bf16 access), a wave holds 64/R rows at once, row statistics by R-lane butterflies (fixed order).
 template <int R>
-__device__ __forceinline__ float grp_sum_r(float v) {
-#pragma unroll
-  for (int o = R / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ float grp_sum_r(float v) { return xl::grp_sum<R>(v); }
 
 template <class T> __device__ __forceinline__ void ld8v(const T* p, float (&v)[8]);
 template <> __device__ __forceinline__ void ld8v<bf16>(const bf16* p, float (&v)[8]) {
@@ -219,11 +211,8 @@ __global__ __launch_bounds__(256) void layernorm8_bwd_kernel(const T* x, const T
   // combine the wave's row groups (lanes with the same channels: xor R, 2R, ...), then the 4 waves in order
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int o = R; o < 64; o <<= 1) {
-      gg[i] += __shfl_xor(gg[i], o, 64);
-      gb[i] += __shfl_xor(gb[i], o, 64);
-    }
+    gg[i] = xl::grp_combine<R>(gg[i]);
+    gb[i] = xl::grp_combine<R>(gb[i]);
   }
   if (sub == 0) {
 #pragma unroll

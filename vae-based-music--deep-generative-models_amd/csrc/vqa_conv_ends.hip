@@ -91,9 +91,7 @@ __global__ __launch_bounds__(256) void co1_fwd_kernel(Co1Args a) {
       for (int k = 0; k < 4; ++k) pk[k] += xj * wr[k][j];
     }
 #pragma unroll
-    for (int m = 1; m < G; m <<= 1)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) pk[k] += __shfl_xor(pk[k], m, 64);
+    for (int k = 0; k < 4; ++k) pk[k] = xl::grp_sum<G>(pk[k]);
     const int lr = p * RPP + rr;
     if (g == 0 && lr < rows_in)
 #pragma unroll

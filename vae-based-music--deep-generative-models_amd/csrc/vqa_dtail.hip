@@ -132,14 +132,6 @@ struct DtArgs {
   int B, T;
 };
 
-// the value of lane ^ 1 / lane ^ 2 by a DPP quad permute (VALU, no LDS crossbar)
-__device__ __forceinline__ float quad_xor1(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ float quad_xor2(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-}
-
 // y[n, 2j + p] for 16 rows per wave and iteration; grid (row blocks, items), grid-stride over the item's rows
 template <class T>
 __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
@@ -190,17 +182,11 @@ __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
       }
       if (j == 0) y0 -= c0;        // out conv padding at t = 0 drops tap k = 0
       if (j == a.T - 1) y1 -= c1;  // ... and at t = 2T - 1 tap k = 2
-#ifdef VQA_DT_DPP
-      y0 += quad_xor1(y0);
-      y1 += quad_xor1(y1);
-      y0 += quad_xor2(y0);
-      y1 += quad_xor2(y1);
-#else
-      y0 += __shfl_xor(y0, 1, 64);
-      y1 += __shfl_xor(y1, 1, 64);
-      y0 += __shfl_xor(y0, 2, 64);
-      y1 += __shfl_xor(y1, 2, 64);
-#endif
+      // the quad's 4 channel slices (DPP quad permutes; see xl in vqa_common.h)
+      y0 += xl::xor1(y0);
+      y1 += xl::xor1(y1);
+      y0 += xl::xor2(y0);
+      y1 += xl::xor2(y1);
       if (j < a.T && q == 0) {
         y0 += bias - (j == 0 ? b0 : 0.f);
         y1 += bias - (j == a.T - 1 ? b2 : 0.f);
@@ -332,11 +318,11 @@ __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
   s[66] = sL;
 #pragma unroll
   for (int e = 0; e < 67; ++e) {
+    // over the lanes of equal q: the row's 4 (rotations by 4 and 8 keep q), then the 4 rows
     float x = s[e];
-    x += __shfl_xor(x, 4, 64);
-    x += __shfl_xor(x, 8, 64);
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
+    x += xl::ror4(x);
+    x += xl::ror8(x);
+    x = xl::sum32(xl::sum16(x));
     s[e] = x;
   }
   if (r == 0) {

@@ -40,16 +40,8 @@ __host__ __device__ inline float prior_uniform(uint64_t seed, uint64_t a, uint64
   return ((float)(uint32_t)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
 }
 
-__device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ float wave_sum_f(float v) { return warp_sum(v); }
+__device__ __forceinline__ float wave_max_f(float v) { return warp_max(v); }
 
 // ---------------------------------------------------------------------------------------------------
 // Sequence-linear layer (MFMA): Y[r][n] = sum_tap sum_k X[src(r, tap)][k] * Wv[tap][k][n] + b[n] (+ R[r][n])
@@ -213,15 +205,16 @@ template <class T> __device__ __forceinline__ uint4 chunk_narrow(const f32x4* v)
 
 // LayerNorm of one row held as the B fragments of a 128-channel row (bf16, lane (row, g) holds channels
 // 32 kc + 8 g .. +7 in fragment kc): the same arithmetic as layernorm8_fwd_kernel<bf16, 16> (vqa_cond.hip) —
-// per-chunk sequential sums, then its butterfly over the 16 chunks (chunk bits 3, 2 are the fragment index
-// bits 1, 0 here; chunk bits 1, 0 are lane bits 5, 4) — so the fused and the unfused forms are bit-identical.
+// per-chunk sequential sums, then its pairwise sums over the 16 chunks, chunk bit 0 first (xl::grp_sum<16>; chunk
+// bits 1, 0 are lane bits 5, 4 here, chunk bits 3, 2 the fragment index bits 1, 0) — so the fused and the unfused
+// forms are bit-identical.
 __device__ __forceinline__ void ln_row_frags(bf16x8 (&x)[4], const float* gs, const float* bs, int g8, float eps) {
   // the bf16 inputs are re-widened per pass (cheap) rather than held as 32 fp32 registers
   auto bfly = [](const float (&c)[4]) {
-    float u = (c[0] + c[2]) + (c[1] + c[3]);
-    u += __shfl_xor(u, 32, 64);
-    u += __shfl_xor(u, 16, 64);
-    return u;
+    float t[4];
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) t[kc] = xl::sum32(xl::sum16(c[kc]));  // chunk bits 0, 1
+    return (t[0] + t[1]) + (t[2] + t[3]);                                 // chunk bits 2, 3
   };
   float s[4];
 #pragma unroll
@@ -361,14 +354,14 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
       }
       return;
     }
-    // lane (row = col, g) holds channels nt*16 + 4g .. +3 -> the wave's fp32 tile; LDS traffic of one wave
-    // is processed in order, so its reads below see these writes
+    // lane (row = col, g) holds channels nt*16 + 4g .. +3 -> the wave's fp32 tile; lds_wave_fence: the writes
+    // have completed before the wave's reads below (and those reads before the next tile's writes)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       if (nt * 16 >= a.N) break;
       *(f32x4*)(E + col * ES + nt * 16 + g4) = acc[nt];
     }
-    __builtin_amdgcn_wave_barrier();
+    lds_wave_fence();
     const int seq = tile / a.tiles_per_seq, tb = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -397,7 +390,7 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
       }
       *yp = chunk_narrow<T>(v);
     }
-    __builtin_amdgcn_wave_barrier();
+    lds_wave_fence();
   };
   typedef std::integral_constant<int, 0> S0;
   typedef std::integral_constant<int, 1> S1;
@@ -713,14 +706,8 @@ struct AttnArgs {
 // raw v_exp_f32 (no denormal range handling: probabilities below 2^-126 flush to zero, as in any softmax)
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-__device__ __forceinline__ float grp_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
-}
-__device__ __forceinline__ float grp_sum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
-}
+__device__ __forceinline__ float grp_max(float v) { return xl::max32(xl::max16(v)); }
+__device__ __forceinline__ float grp_sum(float v) { return xl::sum32(xl::sum16(v)); }
 
 constexpr int AKS = AHD + 4;  // LDS row stride of a 64 x 16 tile (elements)
 
@@ -1299,11 +1286,21 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
     const float mx = grp_max(m[s]);
     const float lt = grp_sum(l[s] * __expf(m[s] - mx));
     // argmax across the four lane groups: larger value, then the lower index
-#pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-      const float ov = __shfl_xor(bv[s], o, 64);
-      const int oi = __shfl_xor(bi[s], o, 64);
-      if (ov > bv[s] || (ov == bv[s] && oi < bi[s])) { bv[s] = ov; bi[s] = oi; }
+    // (the two lanes of each pair, in the same order for the values and the indices; the pick is symmetric)
+    auto pick = [](float av, int ai, float bv2, int bi2, float& v, int& i) {
+      const bool b_wins = bv2 > av || (bv2 == av && bi2 < ai);
+      v = b_wins ? bv2 : av;
+      i = b_wins ? bi2 : ai;
+    };
+    {
+      float av, bv2;
+      int ai, bi2;
+      xl::pair16(bv[s], av, bv2);
+      xl::pair16(bi[s], ai, bi2);
+      pick(av, ai, bv2, bi2, bv[s], bi[s]);
+      xl::pair32(bv[s], av, bv2);
+      xl::pair32(bi[s], ai, bi2);
+      pick(av, ai, bv2, bi2, bv[s], bi[s]);
     }
     const float t = tl[s];
     if (g == 0 && rows[s] < a.M) {

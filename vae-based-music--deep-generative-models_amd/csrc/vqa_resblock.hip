@@ -46,6 +46,8 @@ struct ResArgs {
 
 template <class T> constexpr int rs_stride() { return RC + lds_pad<T>(); }
 constexpr int round16(int v) { return (v + 15) & ~15; }
+// s_waitcnt immediate (gfx9 layout: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]): vmcnt(0) only
+constexpr int kVmcnt0 = 0x0F70;
 
 // ---------------------------------------------------------------------------------------------------
 // Lane maps. Every tile lives in LDS as [row][32 channels] at an 80-byte row stride (bf16). The maps below
@@ -688,6 +690,14 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       if constexpr (DH3 > 0) dh_batch(std::integral_constant<int, DH3>{}, DH1 + DH2);
     }
     __syncthreads();
+#ifndef VQA_RS_LATE_WAIT
+    // The next tile's staged rows (loaded a tile ago) are waited for HERE, before this tile's dx stores are issued.
+    // vmcnt counts loads and stores in one queue: left to the compiler, the wait sits at the rows' register use at the
+    // end of the tile — after team W's dx stores — and, its count merged over both teams' paths, also waits for
+    // those stores' write acknowledgements (s_waitcnt vmcnt(0) there; every wave then idles at the next barrier).
+    // A real s_waitcnt here (the builtin: the compiler's wait pass accounts for it) leaves the later use waitless.
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+#endif
     // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows, NJB n-tiles nt(j) at a time (nt(j) >= NT: none)
     const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
     auto dx_batch = [&](auto nj, auto nt, auto frag) {

@@ -13,6 +13,16 @@
 
 namespace vqa {
 
+// out[r] = v of lane 4 (lane >> 4) + r, for v equal in the wave's 4 rows (row 0's lanes 0-15 serve every group)
+__device__ __forceinline__ void gather_row4(float v, float (&out)[4]) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float a = xl::bcast(v, r), b = xl::bcast(v, 4 + r), c = xl::bcast(v, 8 + r), d = xl::bcast(v, 12 + r);
+    out[r] = g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
+  }
+}
+
 // ---- argmin -------------------------------------------------------------------------------------
 // One workgroup = 4 waves x 32 rows. Distances d = (|z|^2 + |e|^2) - 2 z.e exactly as the reference
 // orders them (VectorQuantizer.py:175-182), in fp32; z.e on v_mfma_f32_16x16x4_f32 (an exact fp32
@@ -39,17 +49,13 @@ __global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const f
       af[rt][ds] = v;
       s += v * v;
     }
-    // full row |z|^2 lives in the 4 lanes {l, l^16, l^32, l^48}
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    zsq[rt] = s;
+    // full row |z|^2: the sum over the 4 lanes {l, l^16, l^32, l^48}
+    zsq[rt] = xl::sum32(xl::sum16(s));
   }
-  // accumulator lane holds rows 4*(lane>>4)+r: fetch their |z|^2 from lane (4*(lane>>4)+r)
+  // accumulator lane holds rows 4*(lane>>4)+r: their |z|^2 from lane (4*(lane>>4)+r)
   float zq[RT][4];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(zsq[rt], 4 * (lane >> 4) + r, 64);
+  for (int rt = 0; rt < RT; ++rt) gather_row4(zsq[rt], zq[rt]);
 
   float best[RT][4];
   int bidx[RT][4];
@@ -101,15 +107,16 @@ __global__ __launch_bounds__(256) void vq_argmin_mfma_kernel(const T* z, const f
     for (int r = 0; r < 4; ++r) {
       float b = best[rt][r];
       int bi = bidx[rt][r];
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {
-        const float ob = __shfl_xor(b, m, 64);
-        const int oi = __shfl_xor(bi, m, 64);
+      auto take = [&](float ob, int oi) {
         if (ob < b || (ob == b && oi < bi)) {
           b = ob;
           bi = oi;
         }
-      }
+      };
+      take(xl::xor1(b), xl::xor1(bi));
+      take(xl::xor2(b), xl::xor2(bi));
+      take(xl::hmirror(b), xl::hmirror(bi));
+      take(xl::mirror(b), xl::mirror(bi));
       const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
       if ((lane & 15) == 0 && row < N) {
         idx[row] = bi;
@@ -189,10 +196,7 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
           const float f = (float)af[rt][ks][j];
           s += f * f;
         }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) zq[rt][r] = __shfl(s, 4 * (lane >> 4) + r, 64);
+      gather_row4(xl::sum32(xl::sum16(s)), zq[rt]);
     }
   };
 #ifdef VQA_ARGMIN_DIST_FORM
@@ -302,15 +306,16 @@ __global__ __launch_bounds__(256) void vq_argmin_split_kernel(const bf16* z, con
     for (int r = 0; r < 4; ++r) {
       float b = best[rt][r];
       int bi = bidx[rt][r];
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {
-        const float ob = __shfl_xor(b, m, 64);
-        const int oi = __shfl_xor(bi, m, 64);
+      auto take = [&](float ob, int oi) {
         if (ob > b || (ob == b && oi < bi)) {
           b = ob;
           bi = oi;
         }
-      }
+      };
+      take(xl::xor1(b), xl::xor1(bi));
+      take(xl::xor2(b), xl::xor2(bi));
+      take(xl::hmirror(b), xl::hmirror(bi));
+      take(xl::mirror(b), xl::mirror(bi));
       const long long row = n0 + rt * 16 + 4 * (lane >> 4) + r;
       if ((lane & 15) == 0 && row < N) {
         // |z|^2 - 2 key (+inf for a row with no finite key). A row with a non-finite |z|^2 has no finite distance
@@ -655,6 +660,7 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t
     __syncthreads();
     if (wv == t && k >= 0) {
       r += hist[k];
+      lds_wave_fence();  // the read has returned before the wave's adds are issued
       w.lrank[row] = r;
       atomicAdd(hist + k, 1);
     }
@@ -704,12 +710,7 @@ __device__ void seg_scan(const int* tot, int* seg, int K) {
   const int per = (K + kSortChunk - 1) / kSortChunk, i0 = min(K, tid * per), i1 = min(K, i0 + per);
   int s = 0;
   for (int i = i0; i < i1; ++i) s += tot[i];
-  int incl = s;  // inclusive wave scan
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
+  const int incl = xl::incl_scan(s);  // inclusive wave scan
   if (lane == 63) wsum[v] = incl;
   __syncthreads();
   int base = 0;

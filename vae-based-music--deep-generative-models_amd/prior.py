@@ -804,14 +804,14 @@ class Prior:
         torch.cuda.synchronize(self.device)
         pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=pool):
+        with torch.cuda.graph(g1, pool=pool, capture_error_mode="thread_local"):
             self._compute(c, u, teacher_force_rate, None, l)
             if not vqa_dp.active(self.process_group):
                 self._apply()
         g2 = None
         if vqa_dp.active(self.process_group):  # two graphs around the eager all_reduce
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=pool):
+            with torch.cuda.graph(g2, pool=pool, capture_error_mode="thread_local"):
                 self._apply()
         self._graph = (g1, g2)
         self._graph_rate = float(teacher_force_rate)

@@ -386,14 +386,14 @@ class VQVAE:
         torch.cuda.synchronize(self.device)
         self._graph_pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=self._graph_pool):
+        with torch.cuda.graph(g1, pool=self._graph_pool, capture_error_mode="thread_local"):
             self._compute(self._graph_x, True)
             if not vqa_dp.active(self.process_group):
                 self._update(True)
         g2 = None
         if vqa_dp.active(self.process_group):
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=self._graph_pool):
+            with torch.cuda.graph(g2, pool=self._graph_pool, capture_error_mode="thread_local"):
                 self._update(True)
         self._graph = (g1, g2)
         torch.cuda.synchronize(self.device)
