@@ -157,7 +157,10 @@ def cpu_baseline(batch, steps, seq):
             "sample": f"oracle torch-CPU fp32 train step (dense one-hot GEMMs, N x K distances, TF-style STFT) on "
                       f"the cfg2 architecture, {batch} x {seq}-frame chunks, {steps} timed steps after 1 warm-up, "
                       f"{threads} threads of {_cpu_model()} (nproc {os.cpu_count()}, {allowed} in this process's "
-                      f"affinity mask, OMP_NUM_THREADS {omp or 'unset'}; {dt:.1f} s)"}
+                      f"affinity mask, OMP_NUM_THREADS {omp or 'unset'}; {dt:.1f} s)",
+            "cores_note": "the GPU box gives one GPU's job a CPU share of 16 threads and sets OMP_NUM_THREADS=16 to "
+                          "say so (its rules: leave that setting and size thread pools to the share); every CPU of "
+                          "the affinity mask is used where no such share is set"}
 
 
 def prior_legs(a, dev, world, rank):

@@ -3,7 +3,8 @@
 Runs Prior.train_step with a torch.distributed process group (gloo, every rank on cuda:0) on its shard of the
 global batch — eager, or as two captured hipGraphs around the eager all_reduce — and saves the state.
     python tests/prior_dp_worker.py MODE OUT   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment)
-MODE: eager | graph, with the suffixes _cond (upsampler form) and / or _drop (dropout 0.1).
+MODE: eager | graph, with the suffixes _cond (upsampler form) and / or _drop (dropout 0.1); VQA_PRIOR_DP_FULL=1:
+config 4's full SMALL_PRIOR (ctx 8192, 2048 bins, depth 6).
 """
 import os
 import sys
@@ -18,7 +19,11 @@ N_LOCAL = 1
 
 
 def cfg():
+    """The short form (ctx 256, 64 bins, depth 3), or with VQA_PRIOR_DP_FULL=1 BASELINE config 4's SMALL_PRIOR
+    itself (ctx 8192, 2048 bins, depth 6; the bench's leg, prior.py:240-335)."""
     from oracle import prior_ref as P
+    if os.environ.get("VQA_PRIOR_DP_FULL") == "1":
+        return P.PriorConfig(bins=2048, ctx=8192, width=128, depth=6, heads=2, blocks=4, attn_stacks=1)
     return P.PriorConfig(bins=64, ctx=256, width=128, depth=3, heads=2, blocks=4, attn_stacks=1)
 
 

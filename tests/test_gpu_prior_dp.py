@@ -34,9 +34,15 @@ def _rel(a, b):
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph", "eager_cond", "graph_cond", "eager_drop", "graph_cond_drop"])
-def test_prior_dp2_matches_single_process(cuda, tmp_path, mode):
+@pytest.mark.parametrize("mode", ["eager", "graph", "eager_cond", "graph_cond", "eager_drop", "graph_cond_drop",
+                                  "eager_full", "graph_full"])
+def test_prior_dp2_matches_single_process(cuda, tmp_path, mode, monkeypatch):
+    """`_full`: BASELINE config 4's SMALL_PRIOR at its own size (ctx 8192, 2048 bins, depth 6), one sequence per
+    rank against one process on both, within the same bounds as the short form."""
     port = _port()
+    full = mode.endswith("_full")
+    mode = mode.replace("_full", "")
+    monkeypatch.setenv("VQA_PRIOR_DP_FULL", "1" if full else "0")
     procs, outs = [], []
     for r in range(2):
         out = str(tmp_path / f"{mode}_rank{r}.pt")

@@ -210,6 +210,12 @@ def cmd_kernel(n, k, streams, ops=("dtail", "resblock", "spectral")):
             bad += 1
             print(f"iteration {key[0]} stream {key[1]}: differing elements dtail {diffs[0]} resblock {diffs[1]} "
                   f"loss {diffs[2]} spectral grad {diffs[3]}", flush=True)
+            if diffs[3]:
+                bad_dr = (o[3] != ref[3]).nonzero()
+                items = sorted(set(bad_dr[:, 0].tolist()))
+                print(f"   spectral grad: items {items}, t {int(bad_dr[:, 1].min())}..{int(bad_dr[:, 1].max())}; first "
+                      f"got / want: {[(round(float(o[3][i, t]), 7), round(float(ref[3][i, t]), 7)) for i, t in bad_dr[:4].tolist()]}",
+                      flush=True)
             if diffs[0]:
                 w = (o[0] != ref[0]).view(B, 2 * T).nonzero()[:8].tolist()
                 print("   dtail (item, t) got / want:", [(i, t, round(float(o[0][i, t, 0]), 5),

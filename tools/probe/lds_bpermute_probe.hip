@@ -6,7 +6,8 @@
 //   bperm_lds  the same shuffles with 256 B of LDS allocated (and touched) by the workgroup
 //   dpp        the same permutations by DPP (quad_perm, row_mirror): VALU, no LDS crossbar
 // The L kernel fills 64 KiB of LDS per workgroup with a pattern, reads it back permuted, counts mismatches.
-//   lds_bpermute_probe VARIANT NSTREAMS_L REPS      (NSTREAMS_L = 0: P alone)
+//   lds_bpermute_probe VARIANT NSTREAMS_L REPS [LDS_KIB]     (NSTREAMS_L = 0: P alone; VARIANT none: L only)
+// LDS_KIB: the L kernel's LDS per workgroup (default 64; gfx950 allows up to 160 KiB per workgroup).
 // P runs on one stream, L on NSTREAMS_L others, concurrently, REPS times; prints wrong P results and L mismatches.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -15,7 +16,7 @@
 #include <vector>
 
 constexpr int ITERS = 2048, BLOCKS = 2048, THREADS = 256;
-constexpr int LWORDS = 16384;  // 64 KiB of LDS per L workgroup
+static int g_lwords = 16384;  // LDS words per L workgroup (power of two)
 
 __device__ __forceinline__ unsigned mix(unsigned x) { x ^= x >> 15; x *= 0x2c1b3c6dU; x ^= x >> 12; return x; }
 static unsigned hmix(unsigned x) { x ^= x >> 15; x *= 0x2c1b3c6dU; x ^= x >> 12; return x; }
@@ -46,15 +47,15 @@ __global__ __launch_bounds__(THREADS) void chain(unsigned* out, unsigned seed) {
   out[blockIdx.x * THREADS + threadIdx.x] = v;
 }
 
-__global__ __launch_bounds__(256) void lds_check(unsigned* bad, int rounds, unsigned seed) {
+__global__ __launch_bounds__(256) void lds_check(unsigned* bad, int rounds, unsigned seed, int lwords) {
   extern __shared__ unsigned L[];
   unsigned miss = 0;
   for (int r = 0; r < rounds; ++r) {
     const unsigned key = seed * 0x9E3779B9u + blockIdx.x * 7919u + (unsigned)r;
-    for (int w = threadIdx.x; w < LWORDS; w += 256) L[w] = mix(key ^ (unsigned)w);
+    for (int w = threadIdx.x; w < lwords; w += 256) L[w] = mix(key ^ (unsigned)w);
     __syncthreads();
-    for (int w = threadIdx.x; w < LWORDS; w += 256) {
-      const int q = (w * 97 + r) & (LWORDS - 1);
+    for (int w = threadIdx.x; w < lwords; w += 256) {
+      const int q = (w * 97 + r) % lwords;
       miss += L[q] != mix(key ^ (unsigned)q);
     }
     __syncthreads();
@@ -65,7 +66,8 @@ __global__ __launch_bounds__(256) void lds_check(unsigned* bad, int rounds, unsi
 int main(int argc, char** argv) {
   const char* var = argc > 1 ? argv[1] : "bperm";
   const int nl = argc > 2 ? atoi(argv[2]) : 2, reps = argc > 3 ? atoi(argv[3]) : 10;
-  const int mode = !strcmp(var, "bperm") ? 0 : !strcmp(var, "bperm_lds") ? 1 : 2;
+  const int mode = !strcmp(var, "bperm") ? 0 : !strcmp(var, "bperm_lds") ? 1 : !strcmp(var, "dpp") ? 2 : 3;
+  if (argc > 4) g_lwords = atoi(argv[4]) * 256;
   const size_t n = (size_t)BLOCKS * THREADS;
   std::vector<unsigned> want(n);
   for (size_t w = 0; w < n / 64; ++w) {
@@ -80,7 +82,7 @@ int main(int argc, char** argv) {
     }
     for (int l = 0; l < 64; ++l) want[w * 64 + l] = v[l];
   }
-  (void)hipFuncSetAttribute((const void*)lds_check, hipFuncAttributeMaxDynamicSharedMemorySize, LWORDS * 4);
+  (void)hipFuncSetAttribute((const void*)lds_check, hipFuncAttributeMaxDynamicSharedMemorySize, g_lwords * 4);
   std::vector<hipStream_t> st(1 + nl);
   for (auto& s : st) (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   unsigned *dp, *dbad;
@@ -91,8 +93,9 @@ int main(int argc, char** argv) {
   long long pbad = 0, pruns = 0;
   for (int r = 0; r < reps; ++r) {
     for (int s = 1; s <= nl; ++s)
-      hipLaunchKernelGGL(lds_check, dim3(1024), dim3(256), LWORDS * 4, st[s], dbad, 1500, (unsigned)(r * 16 + s));
-    for (int k = 0; k < 4; ++k) {
+      hipLaunchKernelGGL(lds_check, dim3(1024), dim3(256), g_lwords * 4, st[s], dbad, 1500, (unsigned)(r * 16 + s),
+                         g_lwords);
+    for (int k = 0; k < (mode == 3 ? 0 : 4); ++k) {
       if (mode == 0) hipLaunchKernelGGL(chain<0>, dim3(BLOCKS), dim3(THREADS), 0, st[0], dp, 1234u);
       if (mode == 1) hipLaunchKernelGGL(chain<1>, dim3(BLOCKS), dim3(THREADS), 0, st[0], dp, 1234u);
       if (mode == 2) hipLaunchKernelGGL(chain<2>, dim3(BLOCKS), dim3(THREADS), 0, st[0], dp, 1234u);
@@ -108,7 +111,7 @@ int main(int argc, char** argv) {
   }
   unsigned lbad = 0;
   (void)hipMemcpy(&lbad, dbad, 4, hipMemcpyDeviceToHost);
-  printf("lds_bpermute_probe %s beside %d LDS streams: %lld P launches, %lld wrong P thread results; "
-         "L mismatches %u\n", var, nl, pruns, pbad, lbad);
+  printf("lds_bpermute_probe %s beside %d LDS streams of %d KiB: %lld P launches, %lld wrong P thread results; "
+         "L mismatches %u\n", var, nl, g_lwords / 256, pruns, pbad, lbad);
   return 0;
 }

@@ -45,10 +45,9 @@ template <> __device__ __forceinline__ void st4<bf16>(bf16* p, f32x4 v) {
 }
 
 // ---- cross-lane moves on the VALU (DPP, v_permlane*_swap, v_readlane) ------------------------------------
-// No kernel of the library uses ds_bpermute_b32 / ds_swizzle (what __shfl* compiles to: the LDS crossbar). On this
-// platform, while kernels of SEVERAL hardware queues share the CUs, ds_bpermute returned wrong data in lanes 48-63
-// of a wave (the decoder tail's row sums) and a spectral kernel's results changed run to run; with these VALU forms
-// both stayed bitwise repeatable (tools/cotenant.py). Every caller below has all 64 lanes active.
+// The library's reductions and lane exchanges use these instead of __shfl* (ds_bpermute_b32 through the LDS
+// crossbar): no LDS instruction, no LDS allocation needed, and — where the values are summed — a fixed pairing
+// whose result is bitwise the same in every lane. Every caller below has all 64 lanes active.
 // Partner helpers return the value of one partner lane; each step of a reduction pairs the two halves of the group
 // the previous steps reduced, so a reduction over a 16-lane row is xor1 -> xor2 -> hmirror -> mirror, and the
 // same fp32 sums are formed in both lanes of every pair (a + b = b + a: every lane ends with identical bits).
@@ -136,16 +135,6 @@ __device__ __forceinline__ int incl_scan(int x) {
 // value of lane `src` (wave-uniform) in every lane
 __device__ __forceinline__ float bcast(float v, int src) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src)); }
 }  // namespace xl
-
-// Every LDS access the wave has issued has completed (reads returned, writes done): s_waitcnt lgkmcnt(0). A wave
-// that rewrites LDS it has just read (or reads what it has just written) without a workgroup barrier calls this
-// between the two: the same run-to-run changes as above (lanes 48-63) showed with in-place LDS passes that relied on
-// the wave's LDS instructions executing in issue order. (gfx9 s_waitcnt layout: vmcnt [3:0] + [15:14] = 63, expcnt
-// [6:4] = 7 — no wait — and lgkmcnt [11:8] = 0.)
-__device__ __forceinline__ void lds_wave_fence() {
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_wave_barrier();
-}
 
 // sum over the 64 lanes, in every lane
 __device__ __forceinline__ float warp_sum(float v) { return xl::sum32(xl::sum16(xl::row_sum(v))); }

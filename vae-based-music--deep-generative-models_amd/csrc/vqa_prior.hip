@@ -354,14 +354,14 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
       }
       return;
     }
-    // lane (row = col, g) holds channels nt*16 + 4g .. +3 -> the wave's fp32 tile; lds_wave_fence: the writes
-    // have completed before the wave's reads below (and those reads before the next tile's writes)
+    // lane (row = col, g) holds channels nt*16 + 4g .. +3 -> the wave's fp32 tile; LDS traffic of one wave
+    // is processed in order, so its reads below see these writes
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       if (nt * 16 >= a.N) break;
       *(f32x4*)(E + col * ES + nt * 16 + g4) = acc[nt];
     }
-    lds_wave_fence();
+    __builtin_amdgcn_wave_barrier();
     const int seq = tile / a.tiles_per_seq, tb = (tile - seq * a.tiles_per_seq) * kSdRows + wave * 16;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
       }
       *yp = chunk_narrow<T>(v);
     }
-    lds_wave_fence();
+    __builtin_amdgcn_wave_barrier();
   };
   typedef std::integral_constant<int, 0> S0;
   typedef std::integral_constant<int, 1> S1;

@@ -237,11 +237,9 @@ __global__ __launch_bounds__(256) void spec_frame_kernel(SpecFrameArgs a) {
 // ONE WAVE PER FRAME PAIR (no workgroup barrier after the table load): each wave owns an LDS buffer of N
 // complex values and runs the Stockham FFT in it with register-resident radix-16 / 8 / 4 / 2 butterflies
 // (2048 = 16.16.8, 1024 = 16.16.4, 512 = 8.8.8, 256 = 16.16: three passes instead of the four to six of a
-// radix-8 / radix-4 plan). A pass loads every input of the lane's butterflies, waits for those loads to
-// return (lds_wave_fence: s_waitcnt lgkmcnt(0)), then stores its outputs, so the passes run IN PLACE in one
-// buffer with no workgroup barrier between them. (Relying on the wave's LDS instructions executing in issue order
-// alone, without the wait, gave results that changed run to run while other queues' kernels shared the CUs:
-// DESIGN.md §5.) The first forward pass reads the windowed samples straight from HBM
+// radix-8 / radix-4 plan). A pass loads every input of the lane's butterflies before it stores an output, and
+// all lanes of a wave execute each LDS instruction together (in order), so the passes run IN PLACE in one
+// buffer with no barrier between them. The first forward pass reads the windowed samples straight from HBM
 // (lane j of butterfly j takes samples j + r N/R: coalesced), the last inverse pass writes the windowed frame
 // gradients straight to HBM (samples q + S k: coalesced); the next pair's samples and target magnitudes are
 // prefetched into registers while the current pair is transformed.
@@ -366,7 +364,7 @@ template <int R, bool INV> __device__ __forceinline__ void pass_twiddles(f32x2 (
 
 // one Stockham pass of radix R at stride S over the wave's buffer z (in place): butterfly j = q + S p reads
 // z[q + S (p + r m)] and writes z[q + S (R p + k)] = W_N^{k p S} DFT_R(...)_k. Every load of the lane precedes
-// its first store (lds_wave_fence between them: every load returned before the first store is issued).
+// its first store (all lanes of the wave execute each LDS instruction together).
 template <int N, int R, int S, bool INV>
 __device__ __forceinline__ void wpass(f32x2* z, const f32x2* tw, int lane) {
   constexpr int m = N / (S * R), NBF = N / R, IT = (NBF + 63) / 64;
@@ -380,7 +378,7 @@ __device__ __forceinline__ void wpass(f32x2* z, const f32x2* tw, int lane) {
       for (int r = 0; r < R; ++r) v[it][r] = z[pidx(q + S * (p + r * m))];
     }
   }
-  lds_wave_fence();  // every load of the pass has returned before its first store
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int j = lane + 64 * it;
@@ -393,7 +391,8 @@ __device__ __forceinline__ void wpass(f32x2* z, const f32x2* tw, int lane) {
       for (int k = 0; k < R; ++k) z[pidx(q + S * (R * p + k))] = k ? cmul(v[it][k], w[k]) : v[it][k];
     }
   }
-  lds_wave_fence();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
 
 template <int N, int MODE>
@@ -467,7 +466,8 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
         for (int k = 0; k < R0; ++k) z[pidx(R0 * p + k)] = k ? cmul(v[k], w[k]) : v[k];
       }
     }
-    lds_wave_fence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
     if (pp + nw < npairs) load_samples(pp + nw);  // lands during this pair's remaining passes
     wpass<N, R1, S1, false>(z, tw, lane);
     if constexpr (R2 > 0) wpass<N, R2, S2, false>(z, tw, lane);
@@ -526,7 +526,8 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
       }
     }
     if constexpr (GRAD) {
-      lds_wave_fence();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
       // inverse FFT: passes 0 .. P-2 in LDS, the last pass straight to the frame gradients (windowed)
       constexpr int RL = R2 > 0 ? R2 : R1, SL = R2 > 0 ? S2 : S1, NBFL = N / RL, ITL = (NBFL + 63) / 64;
       wpass<N, R0, 1, true>(z, tw, lane);
@@ -559,7 +560,8 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
       }
     }
     // the next pair's pass 0 rewrites z: every read of it above precedes those stores in the wave's order
-    lds_wave_fence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   }
 }
 

@@ -660,7 +660,6 @@ __global__ __launch_bounds__(kSortChunk) void vq_sort_count_kernel(const int64_t
     __syncthreads();
     if (wv == t && k >= 0) {
       r += hist[k];
-      lds_wave_fence();  // the read has returned before the wave's adds are issued
       w.lrank[row] = r;
       atomicAdd(hist + k, 1);
     }
