@@ -5,9 +5,8 @@ the global batch — eager, or as the two captured hipGraphs around the eager al
 `vqvaes[0](x, training=True)` forward (the EMA on global statistics), and saves the resulting state.
     python tests/dp_worker.py MODE OUT [CONFIG [DTYPE]]   (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set)
 CONFIG "cfg1" is BASELINE config 1's architecture; "cfg2_short" is the benched architecture (config 2/3: 3
-levels, K = 2048, down_depth [3,2,2]) on an 8192-frame chunk. The ranks run at the same time on the one GPU; the
-tests start them with VQA_LEVEL_STREAMS=0 (each rank's levels on one stream; DESIGN.md §5: two processes on one
-GPU, one of them with several queues active, corrupt single kernels on this platform).
+levels, K = 2048, down_depth [3,2,2], the levels on concurrent streams) on an 8192-frame chunk. The ranks run at the
+same time on the one GPU.
 """
 import os
 import sys

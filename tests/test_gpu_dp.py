@@ -55,12 +55,11 @@ def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False, batch=2, pha
     procs, outs = [], []
     for r in range(world):
         out = str(tmp_path / f"{mode}_{config}_{dtype}_rank{r}.pt")
-        # the ranks share the one test GPU and run at the same time, each with its levels on one stream: two
-        # processes on one GPU while one of them has several queues active get single kernels' results corrupted on
-        # this platform (tools/cotenant.py); the product's DP has one process per GPU
+        # the ranks share the one test GPU and run at the same time, each with its levels on concurrent streams
+        # (with packed FP32 instructions in the kernels, exactly this setting changed results run to run)
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), VQA_DP_PROBE="1" if probe else "0", VQA_DP_BATCH=str(batch),
-                   VQA_DP_PHASES=phases, VQA_LEVEL_STREAMS="0")
+                   VQA_DP_PHASES=phases)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out, config, dtype],
                                       env=env))
         outs.append(out)

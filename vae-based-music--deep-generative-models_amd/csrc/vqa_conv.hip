@@ -780,11 +780,12 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
 
   auto run_tile = [&](int tile) {
     const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
+    // the accumulators start at the bias (the fused residual block's convs do the same: bit-identical outputs)
     f32x4 acc[MT][NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NT; ++j) acc[i][j] = bias[i];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {  // K <= 4 (host-checked): unrolled, uniform exit
       if (k >= a.K) break;
@@ -813,7 +814,7 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
       for (int mt = 0; mt < MT; ++mt) {
         const int o = mt * 16 + 4 * (lane >> 4);
         const int eidx = tl * O + o;
-        f32x4 v = acc[mt][nt] + bias[mt];
+        f32x4 v = acc[mt][nt];
         if (do_mask) {
           const f32x4 m = ld4(ml + eidx);
 #pragma unroll

@@ -456,7 +456,7 @@ void resblock_fwd_kernel(ResArgs a) {
       f32x4 acc[3][2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) rb[j] = min(wave + 4 * j, HR / 16 - 1) * 16;
-      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d);
+      conv_multi<T, true, kRsFwdKperm, false, 3>(acc, wa_frag, X, rb, d, bav[0], bav[1]);  // bias-initialised
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= HR / 16) continue;
@@ -464,8 +464,7 @@ void resblock_fwd_kernel(ResArgs a) {
         const bool live = interior || (r >= 0 && r < a.T);
         if constexpr (sizeof(T) == 2) {
           // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8
-          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
-                                                                                            acc[j][1] + bav[1]))));
+          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0], acc[j][1]))));
           if (!interior && !live) u = uint4{0u, 0u, 0u, 0u};
           *(uint4*)(H + i * XS + oc) = u;
           // the tile's own rows 1..RT (rows >= T dropped by the range check)
@@ -477,7 +476,7 @@ void resblock_fwd_kernel(ResArgs a) {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            v[mt] = acc[j][mt] + bav[mt];
+            v[mt] = acc[j][mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
@@ -498,14 +497,14 @@ void resblock_fwd_kernel(ResArgs a) {
     {
       const __amdgpu_buffer_rsrc_t yr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
       f32x4 acc[NJ][2];
-      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1);
+      conv_multi<T, false, kRsFwdKperm, false, NJ>(acc, wb_frag, H, ry, 1, bbv[0], bbv[1]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (wave + 4 * j >= NT) continue;
         const int tl = ry[j] + pn;
         f32x4 x0, x1;
         xres[j].unpack(x0, x1);
-        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + (acc[j][0] + bbv[0]), x1 + (acc[j][1] + bbv[1]));
+        st8_buf<T>(yr, ((t0 + tl) * RC + oc) * (int)sizeof(T), x0 + acc[j][0], x1 + acc[j][1]);
       }
     }
     if (tile + 1 < tend) __syncthreads();  // every read of H done; the next tile's X is in LDS
@@ -600,7 +599,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < NJB; ++j) rh[j] = min(wave + 4 * (j0 + j), nht - 1) * 16;
       f32x4 acc[NJB][2];
-      conv_multi<T, false, true, false, NJB>(acc, [&](int k, int mt, int sc) { return wfa[k][mt][sc]; }, X, rh, d);
+      conv_multi<T, false, true, false, NJB>(acc, [&](int k, int mt, int sc) { return wfa[k][mt][sc]; }, X, rh, d,
+                                             bav[0], bav[1]);  // bias-initialised, as the forward
       if constexpr (sizeof(T) == 2) {
         // round, then ReLU on the bf16 bits (identical to ReLU then round): 4 cvt + 4 packed max per 8; the
         // SAME-padding rows of an edge tile are zeroed on a separate (wave-uniform) path
@@ -609,8 +609,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           for (int j = 0; j < NJB; ++j) {
             if (wave + 4 * (j0 + j) >= nht) continue;
             const int i = rh[j] + pn;
-            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0] + bav[0],
-                                                                                              acc[j][1] + bav[1]))));
+            uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0], acc[j][1]))));
             if constexpr (decltype(edge)::value) {
               const int r = t0 - d + i;
               if (r < 0 || r >= a.T) u = uint4{0u, 0u, 0u, 0u};
@@ -629,7 +628,7 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
           f32x4 v[2];
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) {
-            v[mt] = acc[j][mt] + bav[mt];
+            v[mt] = acc[j][mt];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[mt][q] = live ? fmaxf(v[mt][q], 0.f) : 0.f;
           }
