@@ -80,7 +80,39 @@ def stage(base, new):  # staging ds_write_b128: lane e -> (row, chunk)
     return cost(W128, lanes, 32)
 
 
+def sw_off(r, c):  # DMA layout of resblock_bwd_dma_kernel (bytes): 64-byte rows, per-16-row-block permutation
+    return ((r & ~3) << 6) + (((r & 3) ^ (c & 1)) << 6) + ((c ^ ((r >> 2) & 3)) << 4)
+
+
+def dma_layout():
+    """bijection check of one 16-row block, the DMA lane -> (row, chunk) map, and the read costs on the layout"""
+    slots = sorted(sw_off(r, c) // 16 for r in range(16) for c in range(4))
+    assert slots == list(range(64)), "layout is not a permutation of the block"
+    for l in range(64):  # lane l of a DMA instruction lands in slot l: its (row, chunk) must map back to slot l
+        s_, dc = l >> 4, (l & 3) ^ (l >> 4)
+        du = ((l >> 2) & 3) ^ (dc & 1)
+        assert sw_off(4 * s_ + du, dc) == 16 * l, l
+    frag = max(cost(B128, [[sw_off(b + pi(l & 15), sig(l >> 4)) // 4 + i for i in range(4)] for l in range(64)], 64)
+               for b in range(32))
+    trc = 0
+    for b in range(32):
+        for c0 in (0, 2):
+            t = 0
+            for h in range(2):
+                lanes = []
+                for l in range(64):
+                    i, g = l & 15, l >> 4
+                    r = b + 2 * (4 * (g & 1) + (i >> 2)) + (g >> 1) + 16 * h
+                    a = (sw_off(r, c0 + ((i & 3) >> 1)) + 8 * (i & 1)) // 4
+                    lanes.append([a, a + 1])
+                t += cost(HALVES, lanes, 64)
+            trc = max(trc, t)
+    return frag, trc
+
+
 def main():
+    f, t = dma_layout()
+    print(f"DMA layout (64-byte rows): fragment ds_read_b128 {f} (ideal 4), tr reads lo+hi {t} (ideal 4)")
     bases = range(16)
     print(f"{'pattern':28s} {'old':>4s} {'new':>4s} {'ideal':>5s}   (LDS-array cycles per wave-instruction)")
     rows = [

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a variant libvqa.so in which only the listed sources get extra compile flags (the other objects are the
-# product build's). Usage: tools/mkvar.sh NAME "EXTRA FLAGS" src1.hip [src2.hip ...]  ->  variants/NAME.so
+# product build's, with the Makefile's flags). Usage: tools/mkvar.sh NAME "EXTRA FLAGS" src1.hip [src2.hip ...]  ->  variants/NAME.so
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; FLAGS=$2; shift 2
@@ -13,8 +13,9 @@ objs=""
 for o in $B/*.o; do
   src=$(basename $o .o).hip
   if [[ " $* " == *" $src "* ]]; then
-    /opt/rocm/bin/hipcc $FLAGS --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
-      -Iinclude -mllvm -amdgpu-mfma-vgpr-form=1 -c $C/$src -o $VB/$(basename $o) &
+    sched=""; [[ $src == vqa_resblock.hip ]] && sched="-mllvm -amdgpu-sched-strategy=max-memory-clause"
+    /opt/rocm/bin/hipcc $FLAGS $sched -Xclang -target-feature -Xclang -packed-fp32-ops --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+      -Iinclude -mllvm -amdgpu-mfma-vgpr-form=1 -c $C/$src -o $VB/$(basename $o) 2> >(grep -v 'packed-fp32-ops' >&2) &
     objs="$objs $VB/$(basename $o)"
   else
     objs="$objs $o"
