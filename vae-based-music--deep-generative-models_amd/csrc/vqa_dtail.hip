@@ -128,9 +128,19 @@ struct DtArgs {
   float* y;         // forward: (B, 2T) fp32
   void* dh;         // backward: (B, T, 32)
   const float* comp;
-  float* part;      // backward: [gridDim.x][DT_PART]
+  float* part;      // backward: one DT_PART row per workgroup (row order: dt_part_row)
   int B, T;
+  int pgroups;      // backward: > 0 -> partial rows laid out [rows / pgroups][pgroups] for the two-stage reduction
 };
+
+// Partial row of workgroup p among P: with G = pgroups > 0 the rows are stored [P / G][G] (row p at (p mod R) G +
+// p / R, R = P / G), so that reducing the buffer as R rows of G DT_PART-wide rows sums each group g's workgroups
+// g R .. g R + R - 1 in order (stage 1, R-deep instead of P-deep), and the G group sums are then reduced in order.
+__device__ __forceinline__ int dt_part_row(int p, int P, int G) {
+  if (G <= 0) return p;
+  const int R = P / G;
+  return (p % R) * G + p / R;
+}
 
 // y[n, 2j + p] for 16 rows per wave and iteration; grid (row blocks, items), grid-stride over the item's rows
 template <class T>
@@ -330,7 +340,8 @@ __global__ __launch_bounds__(256) void dtail_bwd_kernel(DtArgs a) {
     for (int e = 0; e < 67; ++e) red[wave][q][e] = s[e];
   }
   __syncthreads();
-  float* out = a.part + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * DT_PART;
+  float* out = a.part + (size_t)dt_part_row(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, a.pgroups) *
+                           DT_PART;
   for (int e = threadIdx.x; e < DT_PART; e += 256) {
     // element e of the partial row -> (q, slice index)
     int qq, si;
@@ -411,6 +422,8 @@ __global__ __launch_bounds__(256) void dtail_chain_kernel(const float* red, cons
 // grid (gx, B): gx row blocks per item (rows_per_block rows per block and iteration: the forward's 4 waves x 16 x
 // U = 3 = 192, the backward's 4 x 16 x U = 2 = 128), about 1024 workgroups in all (4 resident per CU); one partial
 // row per workgroup in the backward
+constexpr int kDtGroups = 16;  // stage-1 groups of the backward's partial-row reduction
+
 static int dt_gx(int B, int T, int rows_per_block) {
   const int per_item = (T + rows_per_block - 1) / rows_per_block;
   int gx = 1024 / B;
@@ -432,8 +445,8 @@ extern "C" size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype) {
   (void)C;
   (void)Cu;
   (void)dtype;
-  const size_t g = (size_t)dt_gx(B, T, 128) * B;  // the backward's partial rows
-  return ((size_t)DT_COMP + (size_t)DT_PART + g * DT_PART) * sizeof(float);
+  const size_t g = (size_t)dt_gx(B, T, 128) * B;  // the backward's partial rows (+ the stage-1 group sums)
+  return ((size_t)DT_COMP + (size_t)DT_PART + (g + kDtGroups) * DT_PART) * sizeof(float);
 }
 
 extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up, const float* w_out,
@@ -449,7 +462,7 @@ extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up
   hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
-  DtArgs a{h, nullptr, y, nullptr, comp, nullptr, B, T};
+  DtArgs a{h, nullptr, y, nullptr, comp, nullptr, B, T, 0};
   const dim3 g(dt_gx(B, T, 192), B);
   if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_fwd_kernel<bf16>, g, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dtail_fwd_kernel<float>, g, dim3(256), 0, s, a);
@@ -474,12 +487,23 @@ extern "C" int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, 
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
   const dim3 g(dt_gx(B, T, 128), B);
-  DtArgs a{h, dy, nullptr, dh, comp, part, B, T};
+  // many partial rows of few columns: reduced in two fixed-order stages (a single 1024-deep pass over 2 column
+  // blocks was a 23 us serial chain of row loads at the head of every level's backward)
+  const int P = (int)(g.x * g.y), G = (P >= 4 * kDtGroups && P % kDtGroups == 0) ? kDtGroups : 0;
+  float* stage1 = part + (size_t)P * DT_PART;
+  DtArgs a{h, dy, nullptr, dh, comp, part, B, T, G};
   if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_bwd_kernel<bf16>, g, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dtail_bwd_kernel<float>, g, dim3(256), 0, s, a);
   VQA_LAUNCHED("dtail_bwd_kernel");
-  const vqa_partials_desc d{part, red, nullptr, (int)(g.x * g.y), DT_PART, DT_PART, 0};
-  if (int rc = vqa_reduce_partials(&d, 1, stream)) return rc;
+  if (G > 0) {
+    const vqa_partials_desc d1{part, stage1, nullptr, P / G, G * DT_PART, G * DT_PART, 0};
+    if (int rc = vqa_reduce_partials(&d1, 1, stream)) return rc;
+    const vqa_partials_desc d2{stage1, red, nullptr, G, DT_PART, DT_PART, 0};
+    if (int rc = vqa_reduce_partials(&d2, 1, stream)) return rc;
+  } else {
+    const vqa_partials_desc d{part, red, nullptr, P, DT_PART, DT_PART, 0};
+    if (int rc = vqa_reduce_partials(&d, 1, stream)) return rc;
+  }
   const int nbo = (3 * Cu + 3) / 4, nbu = (4 * Cu * DT_C + Cu + 1 + 255) / 256;
   hipLaunchKernelGGL(dtail_chain_kernel, dim3(nbo + nbu), dim3(256), 0, s, red, w_up, b_up, w_out, Cu, nbo, dw_up,
                      db_up, dw_out, db_out);
