@@ -1178,6 +1178,10 @@ template <class T> struct RsFwd {
 template <class T> struct RsBwd {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D>; }
 };
+// the 128-row tile plan of d <= 9 (shorter launches: whole rounds of tiles per workgroup, see bwd_rt_for)
+template <class T> struct RsBwd128 {
+  template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D, (D > 0 && D <= 9) ? 128 : rs_bwd_rt(D)>; }
+};
 
 
 template <class F> static const void* rs_pick(int d) {
@@ -1192,6 +1196,15 @@ template <class F> static const void* rs_pick(int d) {
 
 static int fwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_fwd_rt(d) : RTM; }
 static int bwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_bwd_rt(d) : RTM; }
+#ifndef VQA_RS_RT128_BELOW
+#define VQA_RS_RT128_BELOW 8192
+#endif
+// rows per backward tile for a launch: d <= 9 items shorter than VQA_RS_RT128_BELOW rows use 128-row tiles (whole
+// 2-tile rounds per workgroup: 0.4-1.0 us faster per launch at T = 1024-4096; slower from T = 8192, where
+// 160-row tiles keep less halo per row; profiles/r5_resblock_dma.txt)
+static int bwd_rt_for(int d, int T) {
+  return (d == 1 || d == 3 || d == 9) && T < VQA_RS_RT128_BELOW ? 128 : bwd_rt_of(d);
+}
 
 static void plan(ResArgs& a, int per_cu, int rt, int min_tiles = 1) {
   a.ntm = (a.T + rt - 1) / rt;
@@ -1282,12 +1295,15 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
     (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(256), args, lds, s);
     VQA_LAUNCHED("resblock_bwd_dma_kernel");
   } else {
-    plan(a, kResPerCU, bwd_rt_of(dilation), kResMinTiles);
+    const int rt = bwd_rt_for(dilation, T);
+    plan(a, kResPerCU, rt, kResMinTiles);
     a.part_b = a.part_a + (size_t)a.nwg * E;
-    const size_t lds = bwd_lds(dilation, esz, bwd_rt_of(dilation));
+    const size_t lds = bwd_lds(dilation, esz, rt);
     size_t lds_max = bwd_lds(RMAXD, esz, RTM);  // one reservation for every dilation (the largest plan)
     for (int dd : {1, 3, 9, 27}) lds_max = std::max(lds_max, bwd_lds(dd, esz, rs_bwd_rt(dd)));
-    const void* fn = dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation);
+    const void* fn = rt != bwd_rt_of(dilation)
+                         ? (dtype == VQA_BF16 ? rs_pick<RsBwd128<bf16>>(dilation) : rs_pick<RsBwd128<float>>(dilation))
+                         : (dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation));
     if (int rc = set_lds(fn, lds_max)) return rc;
     void* args[] = {&a};
     (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(256), args, lds, s);
