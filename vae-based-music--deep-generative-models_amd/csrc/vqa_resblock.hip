@@ -237,11 +237,12 @@ struct Rows32Buf {
   int goff[PV], loff[PV];  // byte offset from the tile's first row; LDS element offset from the buffer
   // chunks past the tile's rows load zeros (out-of-range offset) and store them to a trash slot `trash`
   // elements from the buffer: every lane stores, so the staging needs no EXEC-masked branches
-  __device__ __forceinline__ void init(int nrows, int trash) {
+  __device__ __forceinline__ void init(int nrows, int trash, int tid = -1) {
     constexpr int XS = RC + 16 / (int)sizeof(T);
+    if (tid < 0) tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
-      const int e = threadIdx.x + i * NTH;
+      const int e = tid + i * NTH;
       int rr, q;
       if constexpr (CPR == 4) {
         const int G = e >> 3;
@@ -549,8 +550,11 @@ void resblock_fwd_kernel(ResArgs a) {
 //   team H (2, 3)  dh = conv_b^T(dy) * (h > 0) -> D (its own buffer);                then dW_a from X, D
 // Barriers per tile: H ready, D ready, every read done (then the next tile's staged rows are stored), the
 // stored rows visible: four (the one-buffer form needs five).
-template <class T, int DT, int RT = rs_bwd_rt(DT)>
-__global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
+// HALVES = 2: a 512-thread workgroup whose two 4-wave halves run the same pipeline on their own tiles (even / odd
+// offsets of the workgroup's range, each half its own LDS region) and add their weight gradients through LDS at the
+// end in a fixed order: ONE partial row per two tile streams (half the partial-row bytes of two workgroups)
+template <class T, int DT, int RT = rs_bwd_rt(DT), int HALVES = 1>
+__global__ __launch_bounds__(256 * HALVES) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
   constexpr int NW = 4;
   constexpr int XS = rs_stride<T>(), NT = RT / 16;
@@ -567,15 +571,26 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   constexpr int PVY = ((HRM + 2) * RC * (int)sizeof(T) / 16 + 64 * NW - 1) / (64 * NW);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int d = DT > 0 ? DT : a.d, HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
-  T* X = (T*)smem;     // local j <-> row t0 - 2d + j: relu(x)
+  const int wave_g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = HALVES > 1 ? wave_g >> 2 : 0;
+  // each half's LDS region: X, Y, H, D and the trash row (bwd_lds), 16-byte aligned
+  const int half_elems = ((XR + YR + 2 * HR + 1) * XS * (int)sizeof(T) + 15) / 16 * 16 / (int)sizeof(T);
+  T* X = (T*)smem + half * half_elems;  // local j <-> row t0 - 2d + j: relu(x)
   T* Y = X + XR * XS;  // local m <-> row t0 - d - 1 + m (dy)
   T* H = Y + YR * XS;  // local i <-> row t0 - d + i: relu(h)
   T* D = H + HR * XS;  // local i <-> row t0 - d + i: dh
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wave = wave_g & 3, lane = threadIdx.x & 63;  // wave within the half's pipeline
   const int team = wave >> 1, tw = wave & 1;  // team 0 = W, 1 = H; tw = the pair's input-channel tile
   const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
             tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
+  // this half's tiles: tbeg + half, + HALVES, ...; every half runs niter iterations (barriers are workgroup-wide),
+  // computing only while its tile exists
+  const int niter = (tend - tbeg + HALVES - 1) / HALVES;
+  auto adv = [&](RsCursor& c) {
+#pragma unroll
+    for (int h = 0; h < HALVES; ++h) c.next(a.ntm);
+  };
   // conv_a's forward fragments (recompute h) on every wave; team W: conv_a^T (dx), team H: conv_b^T (dh)
   typename M::frag wfa[3][2][rs_ncc<T>()], wt[3][2][rs_ncc<T>()];
   load_wfrags<T, true>(wfa, a.wa);
@@ -600,21 +615,25 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
   };
   Rows32Buf<T, PVX> nx;
   Rows32Buf<T, PVY> ny;
-  nx.init(XR, (XR + YR + 2 * HR) * XS);  // trash row after D
-  ny.init(YR, (YR + 2 * HR) * XS);
+  nx.init(XR, (XR + YR + 2 * HR) * XS, (int)(threadIdx.x & 255));  // trash row after D
+  ny.init(YR, (YR + 2 * HR) * XS, (int)(threadIdx.x & 255));
   RsCursor cur, ldc;
-  cur.set(tbeg, a.ntm);
+  cur.set(min(tbeg + half, tend - 1), a.ntm);
   ldc = cur;
-  load_tile(nx, ny, ldc);
-  nx.template store<true>(X);
-  ny.template store<false>(Y);
-  if (tbeg + 1 < tend) {
-    ldc.next(a.ntm);
+  if (tbeg + half < tend) {
+    load_tile(nx, ny, ldc);
+    nx.template store<true>(X);
+    ny.template store<false>(Y);
+  }
+  if (tbeg + half + HALVES < tend) {
+    adv(ldc);
     load_tile(nx, ny, ldc);
   }
   __syncthreads();
   auto wt_frag = [&](int k, int mt, int sc) { return wt[k][mt][sc]; };
-  for (int tile = tbeg; tile < tend; ++tile, cur.next(a.ntm)) {
+  for (int it = 0; it < niter; ++it, adv(cur)) {
+    const int tile = tbeg + half + HALVES * it;
+    const bool valid = HALVES == 1 || tile < tend;  // wave-uniform: this half has a tile this iteration
     const int n = cur.n, t0 = cur.tm * RT;
     const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
 #ifdef VQA_RS_STAMPS
@@ -665,12 +684,15 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
         }
       }
     };
-    h_batch(std::integral_constant<int, P1A>{}, 0);
-    if constexpr (P1B > 0) h_batch(std::integral_constant<int, P1B>{}, P1A);
+    if (valid) {
+      h_batch(std::integral_constant<int, P1A>{}, 0);
+      if constexpr (P1B > 0) h_batch(std::integral_constant<int, P1B>{}, P1A);
+    }
     RS_STAMP(1);
     __syncthreads();
     RS_STAMP(2);
-    if (team == 0) {
+    if (!valid) {
+    } else if (team == 0) {
       // 2W. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o] (c in tile tw, every o), db_b[o in tile tw]
 #pragma unroll
       for (int kk = 0; kk < RT; kk += M::KS) {
@@ -756,7 +778,8 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
         st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
       }
     };
-    if (team == 0) {
+    if (!valid) {
+    } else if (team == 0) {
       // 3W. n-tiles tw, tw + 2, ...
       dx_batch(std::integral_constant<int, NA1>{}, [&](int j) { return tw + 2 * j; }, wt_frag);
       dx_batch(std::integral_constant<int, NA2>{}, [&](int j) { return tw + 2 * (NA1 + j); }, wt_frag);
@@ -776,17 +799,38 @@ __global__ __launch_bounds__(256) void resblock_bwd_kernel(ResArgs a) {
       }
     }
     RS_STAMP(6);
-    if (tile + 1 < tend) {
+    if (it + 1 < niter) {
       __syncthreads();  // every read of X, Y, H and D for this tile is done
-      nx.template store<true>(X);
-      ny.template store<false>(Y);
-      if (tile + 2 < tend) {
-        ldc.next(a.ntm);
+      if (tile + HALVES < tend) {
+        nx.template store<true>(X);
+        ny.template store<false>(Y);
+      }
+      if (tile + 2 * HALVES < tend) {
+        adv(ldc);
         load_tile(nx, ny, ldc);
       }
       __syncthreads();
     }
     RS_STAMP(7);
+  }
+  if constexpr (HALVES > 1) {
+    // the two halves' sums of the same gradient slice (same wave index) add in a fixed order: half 0 + half 1
+    __syncthreads();  // every LDS read of the last tiles is done
+    float* xch = (float*)smem + ((wave * 64 + lane) * 28);
+    if (half == 1) {
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) *(f32x4*)(xch + 4 * (3 * o + k)) = gw[o][k];
+      *(f32x4*)(xch + 24) = gb;
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gw[o][k] = gw[o][k] + *(const f32x4*)(xch + 4 * (3 * o + k));
+    gb = gb + *(const f32x4*)(xch + 24);
   }
   // partial rows (team W: dW_b | db_b into part_b; team H: dW_a | db_a into part_a), Keras dW[k][c][o]
   float* pr = (team == 0 ? a.part_b : a.part_a) + (size_t)blockIdx.x * (3 * RC * RC + RC);
@@ -826,11 +870,11 @@ constexpr bool kRsDma = VQA_RS_DMA;
 #ifndef VQA_RS_DMA_MODE
 #define VQA_RS_DMA_MODE 1
 #endif
-constexpr int kRsDmaMode = VQA_RS_DMA_MODE;
+constexpr int kRsDmaMode = VQA_RS_DMA_MODE;  // who issues the next tile's DMA: 0 every wave at tile start, 1 team W after dW_b
 #ifndef VQA_RS_DMA_D27
 #define VQA_RS_DMA_D27 0
 #endif
-constexpr bool kRsDma27 = VQA_RS_DMA_D27;  // d = 27 at 96-row tiles (the DMA plan's LDS) against 128 register-staged  // who issues the next tile's DMA: 0 every wave at tile start, 1 team W after dW_b
+constexpr bool kRsDma27 = VQA_RS_DMA_D27;  // d = 27 at 96-row tiles (the DMA plan's LDS) against 128 register-staged
 typedef int rs_v4i __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int sw_off(int r, int c) {
@@ -1178,6 +1222,10 @@ template <class T> struct RsFwd {
 template <class T> struct RsBwd {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D>; }
 };
+// two tile streams per 512-thread workgroup (HALVES = 2): half the partial rows of the long launches
+template <class T> struct RsBwdPair {
+  template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D, rs_bwd_rt(D), 2>; }
+};
 // the 128-row tile plan of d <= 9 (shorter launches: whole rounds of tiles per workgroup, see bwd_rt_for)
 template <class T> struct RsBwd128 {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D, (D > 0 && D <= 9) ? 128 : rs_bwd_rt(D)>; }
@@ -1202,6 +1250,10 @@ static int bwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? r
 // rows per backward tile for a launch: d <= 9 items shorter than VQA_RS_RT128_BELOW rows use 128-row tiles (whole
 // 2-tile rounds per workgroup: 0.4-1.0 us faster per launch at T = 1024-4096; slower from T = 8192, where
 // 160-row tiles keep less halo per row; profiles/r5_resblock_dma.txt)
+#ifndef VQA_RS_PAIR_FROM
+#define VQA_RS_PAIR_FROM (1 << 30)
+#endif
+constexpr int kRsPairFrom = VQA_RS_PAIR_FROM;  // items of at least this many rows: RsBwdPair
 static int bwd_rt_for(int d, int T) {
   return (d == 1 || d == 3 || d == 9) && T < VQA_RS_RT128_BELOW ? 128 : bwd_rt_of(d);
 }
@@ -1296,17 +1348,21 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
     VQA_LAUNCHED("resblock_bwd_dma_kernel");
   } else {
     const int rt = bwd_rt_for(dilation, T);
-    plan(a, kResPerCU, rt, kResMinTiles);
+    // long launches: one 512-thread workgroup per CU running two tile streams (RsBwdPair), one partial row each
+    const bool pair = dtype == VQA_BF16 && rt == bwd_rt_of(dilation) && T >= kRsPairFrom &&
+                      (dilation == 1 || dilation == 3 || dilation == 9 || dilation == 27);
+    plan(a, pair ? kResPerCU / 2 : kResPerCU, rt, pair ? 2 * kResMinTiles : kResMinTiles);
     a.part_b = a.part_a + (size_t)a.nwg * E;
-    const size_t lds = bwd_lds(dilation, esz, rt);
+    const size_t lds = bwd_lds(dilation, esz, rt) * (pair ? 2 : 1);
     size_t lds_max = bwd_lds(RMAXD, esz, RTM);  // one reservation for every dilation (the largest plan)
     for (int dd : {1, 3, 9, 27}) lds_max = std::max(lds_max, bwd_lds(dd, esz, rs_bwd_rt(dd)));
-    const void* fn = rt != bwd_rt_of(dilation)
+    const void* fn = pair ? rs_pick<RsBwdPair<bf16>>(dilation)
+                     : rt != bwd_rt_of(dilation)
                          ? (dtype == VQA_BF16 ? rs_pick<RsBwd128<bf16>>(dilation) : rs_pick<RsBwd128<float>>(dilation))
                          : (dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation));
-    if (int rc = set_lds(fn, lds_max)) return rc;
+    if (int rc = set_lds(fn, pair ? 2 * lds_max : lds_max)) return rc;
     void* args[] = {&a};
-    (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(256), args, lds, s);
+    (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(pair ? 512 : 256), args, lds, s);
     VQA_LAUNCHED("resblock_bwd_kernel");
   }
   const int nwg = a.nwg;
