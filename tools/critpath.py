@@ -23,6 +23,8 @@ def main():
     p.add_argument("entries", nargs="*")
     p.add_argument("--cycles", type=int, default=200_000)
     p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--levels", type=str, default="", help="only launches on these levels' streams (e.g. 1,2)")
+    p.add_argument("--first", action="store_true", help="only the first matching launch per level and capture")
     a = p.parse_args()
     import vqa_lib
     from bench import CFG2
@@ -44,11 +46,25 @@ def main():
         m = VQVAE((65536, 1), dtype="bf16", device=dev, **CFG2)
         m.compile()
         hits = [0]
+        lv = [int(v) for v in a.levels.split(",") if v != ""]
+        seen = set()
 
         def hook():
-            if sys._getframe(2).f_code.co_name in entries:  # the vqa_lib entry that called stream()
-                hits[0] += 1
-                torch.cuda._sleep(a.cycles)
+            if sys._getframe(2).f_code.co_name not in entries:  # the vqa_lib entry that called stream()
+                return
+            if not torch.cuda.is_current_stream_capturing():  # only the replayed graph carries spins
+                return
+            cur = torch.cuda.current_stream()
+            streams = m._streams or []
+            level = next((i for i, st in enumerate(streams) if st.cuda_stream == cur.cuda_stream), None)
+            if lv and level not in lv:
+                return
+            if a.first:
+                if level in seen:
+                    return
+                seen.add(level)
+            hits[0] += 1
+            torch.cuda._sleep(a.cycles)
 
         vqa_lib.launch_hook = hook if entries else None
         try:
@@ -70,7 +86,8 @@ def main():
     base, _ = run([])
     hit_ms, hits = run(set(a.entries))
     base2, _ = run([])
-    print(f"spin {spin_us:.1f} us; delayed entries {sorted(a.entries)}: {hits} spins captured (incl. the eager step)")
+    print(f"spin {spin_us:.1f} us; delayed entries {sorted(a.entries)} levels {a.levels or 'all'}"
+          f"{' first only' if a.first else ''}: {hits} spins in the graph")
     print(f"step: {base:.3f} / {base2:.3f} ms without, {hit_ms:.3f} ms with -> +{hit_ms - (base + base2) / 2:.3f} ms",
           flush=True)
 
