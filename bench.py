@@ -361,7 +361,9 @@ def main():
                "config": {"workload": "SMALL_VQ_VAE 3-level VQ-VAE train step (BASELINE config 2)",
                           "model": "VQVAE levels=3 latent=64 K=2048 down_depth=[3,2,2] width=32 depth=4 dil=3",
                           "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",
-                          "graph": not a.no_graph, "final_loss": round(loss, 5)},
+                          "graph": not a.no_graph, "final_loss": round(loss, 5),
+                          "exchange": ("per-level, overlapped" if model.overlap_exchange else "one bucket after the join")
+                          if dist.is_initialized() else None},
                "roofline": roof, "cpu_baseline": cpu, **legs}
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

@@ -123,3 +123,44 @@ def test_two_rank_exchange_equals_full_batch_step():
     assert np.allclose(got[a:b], full[a:b], rtol=1e-12, atol=1e-12)
     # losses: the mean of the per-rank means equals the full-batch mean
     assert np.allclose(got[b:] / 2, full[b:], rtol=1e-9)
+
+
+def _regions_worker(rank, world, port, out):
+    """Per-level exchange (vqa_dp.exchange_regions over level_regions + the losses) vs the one-bucket exchange."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "vae-based-music--deep-generative-models_amd"), root]
+    import vqa_dp
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        K, D, L = 64, 4, 3
+        lay = vqa_dp.bucket_layout(1000, [2 * K * D + K] * L, L)
+        regs = vqa_dp.level_regions(lay, [(0, 300), (304, 650), (652, 1000)])
+        g = torch.Generator().manual_seed(100 + rank)
+        bucket = torch.randn(lay["total"], generator=g)
+        one = bucket.clone()
+        vqa_dp.exchange(one)
+        for l in (2, 0, 1):  # any issue order: every rank issues the same one
+            assert vqa_dp.exchange_regions(bucket, regs[l]) == world
+        vqa_dp.exchange_regions(bucket, [lay["losses"]])
+        if rank == 0:
+            out.put((bucket.numpy(), one.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_per_level_exchange_equals_one_bucket():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_regions_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, want = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert np.array_equal(got, want)  # fp32 a + b: any two-rank reduction gives the same bits

@@ -50,16 +50,16 @@ def _port():
     return p
 
 
-def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False, batch=2, phases="all"):
+def _run_ranks(mode, tmp_path, config, dtype, world=2, probe=False, batch=2, phases="all", overlap=False):
     port = _port()
     procs, outs = [], []
     for r in range(world):
-        out = str(tmp_path / f"{mode}_{config}_{dtype}_rank{r}.pt")
+        out = str(tmp_path / f"{mode}_{config}_{dtype}_{'ovl' if overlap else 'one'}_rank{r}.pt")
         # the ranks share the one test GPU and run at the same time, each with its levels on concurrent streams
         # (with packed FP32 instructions in the kernels, exactly this setting changed results run to run)
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), VQA_DP_PROBE="1" if probe else "0", VQA_DP_BATCH=str(batch),
-                   VQA_DP_PHASES=phases)
+                   VQA_DP_PHASES=phases, VQA_DP_OVERLAP="1" if overlap else "0")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, out, config, dtype],
                                       env=env))
         outs.append(out)
@@ -249,6 +249,40 @@ def test_dp2_matches_single_process_global_batch(cuda, tmp_path, mode, config, d
         print("\n".join(rep))
         failures += [f"{phase}: {b}" for b in bad]
     assert not failures, failures
+
+
+def _bitwise_diffs(a, b, where=""):
+    """Every tensor of two snapshots (nested dicts / lists) that differs, with its count of differing elements."""
+    out = []
+    if isinstance(a, dict):
+        for k in a:
+            out += _bitwise_diffs(a[k], b[k], f"{where}/{k}")
+    elif isinstance(a, (list, tuple)):
+        for i, (x, y) in enumerate(zip(a, b)):
+            out += _bitwise_diffs(x, y, f"{where}[{i}]")
+    elif isinstance(a, torch.Tensor):
+        if a.shape != b.shape or not torch.equal(a, b):
+            out.append(f"{where}: {int((a != b).sum()) if a.shape == b.shape else 'shape'}")
+    elif a != b:
+        out.append(f"{where}: {a} != {b}")
+    return out
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_dp2_overlapped_exchange_bitwise_equals_one_bucket(cuda, tmp_path, mode):
+    """VQVAE(overlap_exchange=True) on the benched architecture's bf16 step: each level's gradient range and VQ
+    statistics summed on the level's stream right after its backward (its codebook EMA after that, on the same
+    stream), the losses after the join — against the one-bucket exchange after the join. With two ranks every
+    element's sum is a + b either way, and the EMA / Adam kernels read the same sums, so every phase's state is
+    BITWISE equal. (gloo stages through the host: the graph mode's capture keeps the split graphs; the eager
+    warm-up step runs overlapped.)"""
+    config, dtype = "cfg2_short", "bf16"
+    one = _run_ranks(mode, tmp_path, config, dtype)
+    ovl = _run_ranks(mode, tmp_path, config, dtype, overlap=True)
+    for r in range(2):
+        d = _bitwise_diffs(ovl[r], one[r], f"rank{r}")
+        assert not d, d[:20]
 
 
 @pytest.mark.timeout(600)

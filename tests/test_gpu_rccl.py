@@ -69,6 +69,40 @@ def test_rccl_world1_step_equals_single_process_bitwise(cuda, tmp_path):
 
 
 @pytest.mark.timeout(600)
+def test_rccl_world1_overlapped_exchange_equals_single_process_bitwise(cuda, tmp_path):
+    """VQVAE.overlap_exchange on the RCCL branch: per step one ncclAllReduce per level region (gradient range, VQ
+    statistics), issued straight to the process group's communicator on the exchange stream right after that
+    level's backward, then the losses after the join; in graph mode the collectives are CAPTURED with the step
+    into one hipGraph (no split graphs). One rank: bitwise the single-process step, eager and graph."""
+    out = str(tmp_path / "rccl_ovl.pt")
+    p = subprocess.run([sys.executable, os.path.join(HERE, "rccl_worker.py"), out, "overlap"], env=_rccl_env(),
+                       capture_output=True, text=True, timeout=540)
+    log = p.stdout + p.stderr
+    assert p.returncode == 0, log[-4000:]
+    assert _rccl_lines(log), "no RCCL log line (NCCL_DEBUG=INFO): the nccl backend did not run"
+    res = torch.load(out, weights_only=True)
+    for mode in ("eager", "graph"):
+        dp, single = res[f"{mode}_dp"], res[f"{mode}_single"]
+        regs = dp["regions"]
+        sizes = [b - a for lv in regs[:-1] for a, b in lv] + [regs[-1][1] - regs[-1][0]]
+        # ncclAllReduce issued directly on the process group's communicator (vqa_dp._Rccl; at most the one
+        # torch collective that creates a lazily built communicator goes through torch.distributed);
+        # eager: two steps; graph: the warm-up step and the capture (replays re-issue nothing from the host)
+        calls = dp["direct_calls"]
+        assert len(dp["all_reduce_calls"]) <= 1, dp["all_reduce_calls"]
+        assert sorted(calls) == sorted(sizes * 2), calls
+        assert not single["all_reduce_calls"] and not single["direct_calls"]
+        for k in ("weights", "adam_m", "adam_v", "grads", "stats"):
+            n = int((dp[k] != single[k]).sum())
+            assert n == 0, f"{mode}: {k} differs in {n} elements between the overlapped RCCL path and the single step"
+        for a, b in zip(dp["vq"], single["vq"]):
+            assert a["calls"] == b["calls"]
+            for k in ("embeddings", "m_t", "N_t"):
+                assert torch.equal(a[k], b[k]), f"{mode}: codebook {k} differs"
+        assert dp["results"] == single["results"], f"{mode}: metrics differ"
+
+
+@pytest.mark.timeout(600)
 def test_bench_py_rccl_branch_one_process(cuda):
     """bench.py under torch.distributed.run with one process and VQA_DP_FORCE=1: init_process_group("nccl",
     device_id=...), the split-graph DP step with an RCCL all_reduce per step, barrier + max-over-ranks timing."""

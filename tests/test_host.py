@@ -75,6 +75,32 @@ def test_bucket_layout_cfg2():
     assert sl["m_sumT"] == (0, 131072) and sl["n_sum"] == (131072, 133120) and sl["RT"][1] == stats[0]
 
 
+@pytest.mark.parametrize("cfg", [CFG2, TINY])
+def test_level_regions_partition_the_bucket(cfg):
+    """The overlapped exchange (vqa_dp.level_regions): per level its layers' gradient range and its VQ statistics;
+    the gradient ranges tile [0, P) in level order and contain every parameter of that level, so the per-level
+    sums plus the losses cover exactly the one-bucket exchange."""
+    store = _product_store(cfg)
+    K, D = cfg.num_embeddings, cfg.latent_dim
+    lay = vqa_dp.bucket_layout(store.size, [2 * K * D + K] * cfg.levels, cfg.levels)
+    ranges = vqa_dp.level_param_ranges(store.offsets, cfg.levels)
+    regs = vqa_dp.level_regions(lay, ranges)
+    cover = np.zeros(lay["total"], np.int32)
+    for l, (g, st) in enumerate(regs):
+        for a, b in (g, st):
+            cover[a:b] += 1
+        assert st == lay["stats"][l]
+        for n, (o, sh) in store.offsets.items():
+            if n.startswith((f"enc{l}/", f"dec{l}/")):
+                assert g[0] <= o and o + int(np.prod(sh)) <= g[1], n
+    a, b = lay["losses"]
+    cover[a:b] += 1
+    assert (cover == 1).all()
+    assert regs[0][0][0] == 0 and regs[-1][0][1] == lay["grads"][1]
+    with pytest.raises(ValueError):
+        vqa_dp.level_regions(lay, [ranges[0]] + [(ranges[0][0], r[1]) for r in ranges[1:]])
+
+
 def test_single_rank_dp_helpers():
     assert vqa_dp.world_size() == 1 and vqa_dp.rank() == 0
     assert vqa_dp.global_row_range(1000) == (0, 1000)

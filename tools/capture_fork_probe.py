@@ -1,0 +1,85 @@
+"""Which fork / join pattern of a direct ncclAllReduce survives hipGraph capture? (GPU dev tool, world size 1)
+
+origin -> 3 "level" streams (work, then the level's collective, then more work) -> joined into the origin, captured
+and replayed. Patterns: the collective on one shared exchange stream forked from each level stream in turn
+(temporary events / events kept alive to capture_end), on the level stream itself, or on a per-level stream.
+    python tools/capture_fork_probe.py level|perlevel|keep|shared      (MASTER_ADDR / MASTER_PORT set)
+Measured (round 5, PyTorch 2.10 / ROCm 7.0 / RCCL 2.26.6): "level" captures and replays right; "perlevel", "keep"
+and "shared" segfault in capture_end (profiles/r5_dp_overlap.txt).
+"""
+import faulthandler
+import os
+import sys
+
+faulthandler.enable()
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "vae-based-music--deep-generative-models_amd"), ROOT]
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    pat = sys.argv[1]
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import vqa_dp
+    vqa_dp.FORCE_COLLECTIVE = True
+    r = vqa_dp.rccl_direct(None, dev)
+    xs = [torch.ones(4096, device=dev) * (l + 1) for l in range(3)]
+    lv = [torch.cuda.Stream() for _ in range(3)]
+    per = [torch.cuda.Stream() for _ in range(3)]
+    shared = torch.cuda.Stream()
+    keep = []
+
+    def ev(s):
+        e = torch.cuda.Event()
+        e.record(s)
+        keep.append(e)
+        return e
+
+    def coll(l):
+        x, cur = xs[l], torch.cuda.current_stream()
+        if pat == "level":
+            rc = r.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), 7, 0, r.comm, cur.cuda_stream)
+        else:
+            side = per[l] if pat == "perlevel" else shared
+            if pat == "keep":
+                side.wait_event(ev(cur))
+            else:
+                side.wait_stream(cur)
+            rc = r.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), 7, 0, r.comm, side.cuda_stream)
+            if pat == "keep":
+                cur.wait_event(ev(side))
+            else:
+                cur.wait_stream(side)
+        assert rc == 0
+
+    def step():
+        main = torch.cuda.current_stream()
+        for s in lv:
+            s.wait_stream(main)
+        for l in range(3):
+            with torch.cuda.stream(lv[l]):
+                xs[l].mul_(2)
+        for l in range(3):
+            with torch.cuda.stream(lv[l]):
+                coll(l)
+                xs[l].add_(1)
+        for s in lv:
+            main.wait_stream(s)
+
+    step()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        step()
+    print(pat, "captured", flush=True)
+    g.replay()
+    torch.cuda.synchronize()
+    print(pat, "ok", [float(x[0]) for x in xs], flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -14,7 +14,8 @@ MI355X design: every conv / VQ / loss / optimizer op is a libvqa HIP kernel call
 torch's current stream; the backward is written out explicitly (no autograd tape over the conv stack);
 each level runs forward then backward immediately (levels are independent), so only one level's
 activations are alive. Weights, gradients and the codebook EMA sums are flat fp32 buffers: the whole
-data-parallel exchange is ONE all_reduce (RCCL over xGMI) of [grads | EMA sums | reset rows | losses].
+data-parallel exchange sums [grads | EMA sums | reset rows | losses] over ranks: on RCCL per level as soon as that
+level's backward ends (`overlap_exchange`, vqa_dp.level_regions), on gloo as ONE all_reduce after the join.
 `capture_train_step` records the full step as a hipGraph (torch.cuda.graph) so replay has no host cost.
 """
 from __future__ import annotations
@@ -101,7 +102,8 @@ def get_vqvae(input_shape, encoder, decoder, vq, level=0, **kwargs):
 class VQVAE:
     def __init__(self, input_shape, levels, latent_dim, down_depth, strides, num_embeddings=128, residual_width=64,
                  residual_depth=4, dilation_factor=1, train_variance=1.0, *, dtype="bf16", device="cuda",
-                 seed=1, codebook_seed=2, reset_seed=3, process_group=None, name="vqvae", **kwargs):
+                 seed=1, codebook_seed=2, reset_seed=3, process_group=None, name="vqvae", overlap_exchange=None,
+                 **kwargs):
         self.input_shape = tuple(input_shape)
         self.T = int(self.input_shape[0])
         self.channels = int(self.input_shape[-1]) if len(self.input_shape) > 1 else 1
@@ -114,6 +116,16 @@ class VQVAE:
         self.device = torch.device(device)
         self.name = name
         self.process_group = process_group
+        # data-parallel exchange per level, overlapped with the other levels' chains (vqa_dp): True / False, or None =
+        # VQA_DP_OVERLAP=1 / 0 if set, else on for a device-side backend (RCCL) and off for gloo (host-staged)
+        env = os.environ.get("VQA_DP_OVERLAP")
+        self._overlap_cfg = bool(overlap_exchange) if overlap_exchange is not None else (
+            None if env is None else env == "1")
+        # the order the levels' exchanges are issued in (one communicator: its collectives run in issue order, so
+        # the level whose chain ends first goes first; VQA_DP_OVERLAP_ORDER="0,1,2")
+        self.exchange_order = [int(v) for v in os.environ.get("VQA_DP_OVERLAP_ORDER", ",".join(
+            str(l) for l in range(levels))).split(",")]
+        assert sorted(self.exchange_order) == list(range(levels)), self.exchange_order
 
         self.vqs = [VectorQuantizer(num_embeddings, latent_dim, level=l, name=f"vector_quantizer_{l}",
                                     device=self.device, seed=codebook_seed + 1000 * l, reset_seed=reset_seed)
@@ -149,6 +161,10 @@ class VQVAE:
             vq.bind_stats(self.bucket[a:b])
         self._stats_region = self.bucket[P:]
         self.loss_slots = self.bucket[lay["losses"][0]:lay["losses"][1]].view(levels, 3)
+        self._loss_region = [tuple(lay["losses"])]
+        # each level's slices of the bucket: its layers' gradient range (enc{l}/*, dec{l}/*) and its VQ statistics
+        self.level_regions = vqa_dp.level_regions(lay, vqa_dp.level_param_ranges(self.store.offsets, levels))
+        self._overlapped = False  # did the last _compute exchange per level (then _exchange sums the losses only)
         for l, vq in enumerate(self.vqs):
             vq.commit = self.loss_slots[l, 1:2]
 
@@ -234,12 +250,16 @@ class VQVAE:
         self._stats_region.zero_()
         main = torch.cuda.current_stream(self.device)
         streams = self._level_streams()
+        overlap = self._overlap_now()
+        self._overlapped = overlap
         ema_in_level = not vqa_dp.active(self.process_group) and not self._r3_layout
         if streams is None or self._r3_layout:
             target = SpectralTarget(x)
         if streams is None:
             for l in range(self.levels):
                 self._level_step(x, l, target, training_grads, ema_in_level)
+                if overlap:
+                    self._level_exchange(l, training_grads)
         else:
             for s in streams:
                 s.wait_stream(main)
@@ -251,9 +271,34 @@ class VQVAE:
             for l in range(self.levels):
                 with torch.cuda.stream(streams[l]):
                     self._level_step(x, l, target, training_grads, ema_in_level)
+            if overlap:
+                # every chain is queued before the first collective (a host-staged gloo exchange blocks the host)
+                for l in self.exchange_order:
+                    with torch.cuda.stream(streams[l]):
+                        self._level_exchange(l, training_grads)
             for s in streams:
                 main.wait_stream(s)
         self.store.deferred = None
+
+    @property
+    def overlap_exchange(self) -> bool:
+        if self._overlap_cfg is not None:
+            return self._overlap_cfg
+        return bool(vqa_dp.active(self.process_group) and vqa_dp.device_side(self.process_group))
+
+    def _overlap_now(self) -> bool:
+        """Exchange per level in this _compute? Only on the data-parallel path, and not while a host-staged (gloo)
+        exchange would have to be captured into a graph (capture_train_step then keeps the split graphs)."""
+        if not (self.overlap_exchange and vqa_dp.active(self.process_group)) or self._r3_layout:
+            return False
+        return not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+                    and vqa_dp.host_staged(self.bucket, self.process_group))
+
+    def _level_exchange(self, l: int, grads: bool):
+        """Level l's share of the exchange on the current (level) stream, then its codebook EMA on the sums."""
+        g, st = self.level_regions[l]
+        vqa_dp.exchange_regions(self.bucket, [g, st] if grads else [st], self.process_group)
+        self.vqs[l].apply_ema(update_trackers=False)
 
     def _level_streams(self):
         """One HIP stream per level when `concurrent_levels`: the levels share nothing but the input and
@@ -291,7 +336,8 @@ class VQVAE:
         world = self._world()
         if apply_grads:
             self.optimizer.apply(self.store, grad_scale=1.0 / world)
-        if vqa_dp.active(self.process_group) or self._r3_layout:  # else the levels' chains applied it (_compute)
+        if (vqa_dp.active(self.process_group) and not self._overlapped) or self._r3_layout:
+            # else the levels' chains applied it (_compute)
             for vq in self.vqs:
                 vq.apply_ema(update_trackers=False)
         # update_metrics (vqvae.py:262-304) + the VQ trackers: one launch
@@ -299,7 +345,10 @@ class VQVAE:
 
     def _exchange(self, grads: bool = True):
         """The step's one collective: all_reduce(SUM) of [grads | EMA sums | reset rows | losses]; without
-        gradients (test_step) only the statistics region."""
+        gradients (test_step) only the statistics region. After an overlapped _compute only the losses are left."""
+        if self._overlapped:
+            vqa_dp.exchange_regions(self.bucket, self._loss_region, self.process_group)
+            return
         vqa_dp.exchange(self.bucket if grads else self._stats_region, self.process_group)
 
     def update_metrics(self, level_losses, recon_losses, commit_losses, spectral_losses):
@@ -370,7 +419,8 @@ class VQVAE:
     def capture_train_step(self, x_example, warmup: int = 2):
         """Run `warmup` eager steps (real steps) then record one full train step as a hipGraph; later
         train_step calls with this batch shape copy the batch in and replay. With a process group the
-        step is two graphs around the eager RCCL all_reduce."""
+        step is two graphs around the eager RCCL all_reduce; with `overlap_exchange` on a device-side backend
+        (RCCL) the per-level collectives are captured with the step into one graph."""
         if self.optimizer is None:
             self.compile()
         x = self._as_input(x_example)
@@ -388,10 +438,13 @@ class VQVAE:
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=self._graph_pool, capture_error_mode="thread_local"):
             self._compute(self._graph_x, True)
-            if not vqa_dp.active(self.process_group):
+            one_graph = self._overlapped or not vqa_dp.active(self.process_group)
+            if self._overlapped:
+                self._exchange()
+            if one_graph:
                 self._update(True)
         g2 = None
-        if vqa_dp.active(self.process_group):
+        if not one_graph:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=self._graph_pool, capture_error_mode="thread_local"):
                 self._update(True)
