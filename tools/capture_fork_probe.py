@@ -62,19 +62,31 @@ def main():
         for l in range(3):
             with torch.cuda.stream(lv[l]):
                 xs[l].mul_(2)
+        prev = None
         for l in range(3):
             with torch.cuda.stream(lv[l]):
+                if prev is not None and os.environ.get("PROBE_CHAIN") == "1":
+                    torch.cuda.current_stream().wait_event(prev)
                 coll(l)
+                prev = ev(torch.cuda.current_stream())
                 xs[l].add_(1)
         for s in lv:
             main.wait_stream(s)
 
     step()
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    dot = os.environ.get("PROBE_DOT")
+    g = torch.cuda.CUDAGraph(keep_graph=bool(dot))  # keep the captured hipGraph_t for the dump
     with torch.cuda.graph(g, capture_error_mode="thread_local"):
         step()
     print(pat, "captured", flush=True)
+    if dot:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipGraphDebugDotPrint.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint]
+        raw = g.raw_cuda_graph()
+        rc = hip.hipGraphDebugDotPrint(ctypes.c_void_p(raw), os.path.abspath(dot).encode(), 1 << 0 | 1 << 2)
+        print("hipGraphDebugDotPrint", rc, os.path.abspath(dot), flush=True)
     g.replay()
     torch.cuda.synchronize()
     print(pat, "ok", [float(x[0]) for x in xs], flush=True)

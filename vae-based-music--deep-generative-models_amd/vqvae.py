@@ -165,6 +165,7 @@ class VQVAE:
         # each level's slices of the bucket: its layers' gradient range (enc{l}/*, dec{l}/*) and its VQ statistics
         self.level_regions = vqa_dp.level_regions(lay, vqa_dp.level_param_ranges(self.store.offsets, levels))
         self._overlapped = False  # did the last _compute exchange per level (then _exchange sums the losses only)
+        self._exchange_events: List[torch.cuda.Event] = []
         for l, vq in enumerate(self.vqs):
             vq.commit = self.loss_slots[l, 1:2]
 
@@ -252,6 +253,7 @@ class VQVAE:
         streams = self._level_streams()
         overlap = self._overlap_now()
         self._overlapped = overlap
+        self._exchange_events = []
         ema_in_level = not vqa_dp.active(self.process_group) and not self._r3_layout
         if streams is None or self._r3_layout:
             target = SpectralTarget(x)
@@ -272,10 +274,13 @@ class VQVAE:
                 with torch.cuda.stream(streams[l]):
                     self._level_step(x, l, target, training_grads, ema_in_level)
             if overlap:
-                # every chain is queued before the first collective (a host-staged gloo exchange blocks the host)
+                # every chain is queued before the first collective (a host-staged gloo exchange blocks the host);
+                # each level's collectives wait for the previous level's (an event, not a join of the chains), so
+                # they execute in one order on every rank whatever RCCL does with collectives on concurrent streams
+                prev = None
                 for l in self.exchange_order:
                     with torch.cuda.stream(streams[l]):
-                        self._level_exchange(l, training_grads)
+                        prev = self._level_exchange(l, training_grads, after=prev)
             for s in streams:
                 main.wait_stream(s)
         self.store.deferred = None
@@ -294,11 +299,21 @@ class VQVAE:
         return not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
                     and vqa_dp.host_staged(self.bucket, self.process_group))
 
-    def _level_exchange(self, l: int, grads: bool):
-        """Level l's share of the exchange on the current (level) stream, then its codebook EMA on the sums."""
+    def _level_exchange(self, l: int, grads: bool, after: Optional[torch.cuda.Event] = None):
+        """Level l's share of the exchange on the current (level) stream — after the event `after` (the previous
+        level's collectives) — then its codebook EMA on the sums. Returns the event that follows its collectives."""
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        if after is not None:
+            cur.wait_event(after)
         g, st = self.level_regions[l]
         vqa_dp.exchange_regions(self.bucket, [g, st] if grads else [st], self.process_group)
+        done = None
+        if cur is not None:
+            done = torch.cuda.Event()
+            done.record(cur)
+            self._exchange_events.append(done)  # alive until the next step's exchange (capture_end reads them)
         self.vqs[l].apply_ema(update_trackers=False)
+        return done
 
     def _level_streams(self):
         """One HIP stream per level when `concurrent_levels`: the levels share nothing but the input and
