@@ -103,11 +103,12 @@ def test_rccl_world1_overlapped_exchange_equals_single_process_bitwise(cuda, tmp
 
 
 @pytest.mark.timeout(600)
-def test_bench_py_rccl_branch_one_process(cuda):
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_bench_py_rccl_branch_one_process(cuda, overlap):
     """bench.py under torch.distributed.run with one process and VQA_DP_FORCE=1: init_process_group("nccl",
     device_id=...), the split-graph DP step with an RCCL all_reduce per step, barrier + max-over-ranks timing."""
     env = _rccl_env()
-    env.update(VQA_DP_FORCE="1", OMP_NUM_THREADS="4")
+    env.update(VQA_DP_FORCE="1", OMP_NUM_THREADS="4", VQA_DP_OVERLAP=overlap)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
@@ -120,3 +121,4 @@ def test_bench_py_rccl_branch_one_process(cuda):
     assert len(lines) == 1, p.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1" and out["value"] > 0
+    assert out["config"]["exchange"] == ("per-level, overlapped" if overlap == "1" else "one bucket after the join")

@@ -10,9 +10,9 @@ exactly the single-device step at global batch W*B provided:
     batch (global row = rank * N_local + local row): each rank writes the candidate rows it owns and
     zeros elsewhere                                       -> all_reduce(SUM) assembles R exactly.
 All of it is ONE flat fp32 bucket [grads | per-level (m_sumT, n_sum, RT) | per-level losses], so a step
-can be summed by one collective (the gloo default); with ~7 MB at cfg2 it is latency-bound on xGMI (tens of µs).
+is summed by one collective by default; with ~7 MB at cfg2 it is latency-bound on xGMI (tens of µs).
 
-Overlapped form (the default on RCCL; VQVAE(overlap_exchange=...) / VQA_DP_OVERLAP=0|1): the levels' chains are independent, so each
+Overlapped form (VQVAE(overlap_exchange=True) / VQA_DP_OVERLAP=1; off by default): the levels' chains are independent, so each
 level's share of the bucket — its layers' gradient range and its VQ statistics (`level_regions`) — is summed as
 soon as that level's backward ends, on the level's own stream, while the other levels still compute (SURVEY.md
 §8e: "the all-reduce overlaps with the backward pass of earlier levels"); the level's codebook EMA follows on

@@ -15,7 +15,7 @@ torch's current stream; the backward is written out explicitly (no autograd tape
 each level runs forward then backward immediately (levels are independent), so only one level's
 activations are alive. Weights, gradients and the codebook EMA sums are flat fp32 buffers: the whole
 data-parallel exchange sums [grads | EMA sums | reset rows | losses] over ranks: on RCCL per level as soon as that
-level's backward ends (`overlap_exchange`, vqa_dp.level_regions), on gloo as ONE all_reduce after the join.
+level's backward ends (`overlap_exchange`, vqa_dp.level_regions) or as ONE all_reduce after the join (default).
 `capture_train_step` records the full step as a hipGraph (torch.cuda.graph) so replay has no host cost.
 """
 from __future__ import annotations
@@ -117,10 +117,9 @@ class VQVAE:
         self.name = name
         self.process_group = process_group
         # data-parallel exchange per level, overlapped with the other levels' chains (vqa_dp): True / False, or None =
-        # VQA_DP_OVERLAP=1 / 0 if set, else on for a device-side backend (RCCL) and off for gloo (host-staged)
-        env = os.environ.get("VQA_DP_OVERLAP")
+        # VQA_DP_OVERLAP=1 (off by default: the multi-rank captured form has not run on hardware)
         self._overlap_cfg = bool(overlap_exchange) if overlap_exchange is not None else (
-            None if env is None else env == "1")
+            os.environ.get("VQA_DP_OVERLAP", "0") == "1")
         # the order the levels' exchanges are issued in (one communicator: its collectives run in issue order, so
         # the level whose chain ends first goes first; VQA_DP_OVERLAP_ORDER="0,1,2")
         self.exchange_order = [int(v) for v in os.environ.get("VQA_DP_OVERLAP_ORDER", ",".join(
@@ -287,9 +286,7 @@ class VQVAE:
 
     @property
     def overlap_exchange(self) -> bool:
-        if self._overlap_cfg is not None:
-            return self._overlap_cfg
-        return bool(vqa_dp.active(self.process_group) and vqa_dp.device_side(self.process_group))
+        return self._overlap_cfg
 
     def _overlap_now(self) -> bool:
         """Exchange per level in this _compute? Only on the data-parallel path, and not while a host-staged (gloo)
