@@ -1034,9 +1034,11 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* v)
   *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
 
-template <class TX, class TG, bool WIDE_X>
+// NM: the narrow side's width bound (1 for the model's 1-channel ends: half the accumulators and tap registers of
+// NM = 2, 29.4 vs 33.6 us for the first encoder conv at cfg2, the same sums in the same order)
+template <class TX, class TG, bool WIDE_X, int NM>
 __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
-  constexpr int KM = 4, NM = 2, U = 8;  // max taps, max narrow width, rows in flight per thread
+  constexpr int KM = 4, U = 8;  // max taps, rows in flight per thread
   const int W = WIDE_X ? a.C : a.O;
   const int NN = WIDE_X ? a.O : a.C;
   const int VL = W / 8, RL = 256 / VL;
@@ -1786,14 +1788,19 @@ static int launch_wgrad_direct(const WgradArgs& a, const WgradPlan& p, hipStream
   return VQA_OK;
 }
 
-template <class TX, class TG, bool WX>
-static int launch_wgrad_thin(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+template <class TX, class TG, bool WX, int NM>
+static int launch_wgrad_thin_nm(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
   static size_t lds_set = 0;
-  const int rc = ensure_dyn_lds((const void*)wgrad_thin_kernel<TX, TG, WX>, p.lds, &lds_set, "wgrad_thin_kernel");
+  const int rc = ensure_dyn_lds((const void*)wgrad_thin_kernel<TX, TG, WX, NM>, p.lds, &lds_set, "wgrad_thin_kernel");
   if (rc != VQA_OK) return rc;
-  hipLaunchKernelGGL((wgrad_thin_kernel<TX, TG, WX>), dim3(p.nchunk, a.B), dim3(256), p.lds, s, a);
+  hipLaunchKernelGGL((wgrad_thin_kernel<TX, TG, WX, NM>), dim3(p.nchunk, a.B), dim3(256), p.lds, s, a);
   VQA_LAUNCHED("wgrad_thin_kernel");
   return VQA_OK;
+}
+
+template <class TX, class TG, bool WX>
+static int launch_wgrad_thin(const WgradArgs& a, const WgradPlan& p, hipStream_t s) {
+  return (WX ? a.O : a.C) == 1 ? launch_wgrad_thin_nm<TX, TG, WX, 1>(a, p, s) : launch_wgrad_thin_nm<TX, TG, WX, 2>(a, p, s);
 }
 
 template <bool WX>
