@@ -5,7 +5,9 @@ Workload (BASELINE config 2, "SMALL_VQ_VAE 3-level"): levels 3, latent 64, codeb
 44.1 kHz synthetic chunks, batch 32 per GPU, bf16 activations with fp32 weights / VQ state / Adam.
 A step = one full VQVAE.train_step (forward, spectral + MSE + commitment losses, backward, Keras Adam,
 codebook EMA with dead-code reset), replayed from a hipGraph. N > 1: data parallel (weak scaling), one
-RCCL all_reduce of [grads | EMA sums | reset rows | losses] per step.
+RCCL all_reduce of [grads | EMA sums | reset rows | losses] per step. `--gpus N` is authoritative: a bare
+`python bench.py --gpus N` starts the N ranks itself (a child `torch.distributed.run`, 127.0.0.1 rendezvous);
+under a launcher each rank refuses to run unless WORLD_SIZE == N.
 
 Prints ONE JSON line on rank 0. Also reports:
   roofline     — the dominant kernel (fused residual-block backward) — its algorithmic bytes (SURVEY §8d layer
@@ -234,9 +236,44 @@ def prior_legs(a, dev, world, rank):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """`--gpus N` with N > 1 and no WORLD_SIZE in the environment: this process is only the launcher. It starts
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same arguments>` as a CHILD process (one rank
+    per GPU, rendezvous on 127.0.0.1) and returns its exit code. Nothing here touches the GPU (counting devices
+    does not initialise it), and nothing execs: the ranks are children, the launcher waits."""
+    import subprocess
+    backend = os.environ.get("VQA_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs for RCCL, {have} visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        print(f"bench.py: --gpus must be >= 1 (got {a.gpus})", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        # the rank count comes from the launcher; --gpus must name the same number or the line would mislabel
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; run `bench.py --gpus N` (it starts the N ranks "
+              f"itself) or a launcher with --nproc-per-node equal to --gpus", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # VQA_DIST_BACKEND=gloo + ranks sharing one GPU (local rank wrapped onto the visible devices) rehearses the
@@ -365,11 +402,16 @@ def main():
                           "exchange": ("per-level, overlapped" if model.overlap_exchange else "one bucket after the join")
                           if dist.is_initialized() else None},
                "roofline": roof, "cpu_baseline": cpu, **legs}
+        if dist.is_initialized() and model.overlap_exchange:
+            out["config"]["exchange_note"] = ("VQA_DP_OVERLAP=1 forced the per-level exchange on; its captured "
+                                              "multi-rank form had not run on hardware before this line (DESIGN.md §5)")
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.barrier()
+        import vqa_dp
+        vqa_dp.reset()
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -81,6 +81,12 @@ def run(m, xs, mode):
         res["step1"] = snapshot(m)
         if PHASES == "step1":
             return res
+        if PHASES == "mixed":
+            # an eager test_step between the capture and the next replay: the replay must still exchange the
+            # whole bucket the captured graphs were split around, whatever form the eager step used
+            m.test_step(xs[2])
+            torch.cuda.synchronize()
+            res["test"] = snapshot(m)
         m.train_step(xs[1])
     torch.cuda.synchronize()
     res["steps"] = snapshot(m)

@@ -64,6 +64,7 @@ def main():
             torch.cuda.empty_cache()
     vqa_dp.FORCE_COLLECTIVE = False
     torch.save(res, out)
+    vqa_dp.reset()
     dist.destroy_process_group()
 
 

@@ -286,6 +286,24 @@ def test_dp2_overlapped_exchange_bitwise_equals_one_bucket(cuda, tmp_path, mode)
 
 
 @pytest.mark.timeout(600)
+def test_dp2_graph_replay_after_eager_test_step_overlapped(cuda, tmp_path):
+    """Capture, then an eager test_step, then a replayed train_step, with overlap_exchange on (gloo: the capture
+    keeps the split graphs, the eager test_step runs its exchange per level). The replay must exchange the whole
+    bucket between its two graphs — the form it was captured with, not the form of the eager step before it — so
+    every phase equals the one-bucket run bitwise (before the fix the replay summed only the losses and the ranks'
+    gradients and VQ statistics were never reduced)."""
+    config, dtype = "cfg2_short", "bf16"
+    one = _run_ranks("graph", tmp_path, config, dtype, phases="mixed")
+    ovl = _run_ranks("graph", tmp_path, config, dtype, phases="mixed", overlap=True)
+    for r in range(2):
+        d = _bitwise_diffs(ovl[r], one[r], f"rank{r}")
+        assert not d, d[:20]
+    # and the replicas agree with each other after the replay (a local-only update would split them)
+    d = _bitwise_diffs(ovl[0]["steps"], ovl[1]["steps"], "rank0 vs rank1")
+    assert not d, d[:20]
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("mode", ["eager", "graph"])
 def test_exchange_stream_contract_both_sides(cuda, tmp_path, mode):
     """The stream-ordering contract of `vqa_dp.exchange` on both sides, at the benched architecture's bf16 step
@@ -410,3 +428,23 @@ def test_bench_py_dp2_gloo_one_gpu(cuda):
     assert c4["n_gpus"] == 2 and c4["config"]["parallelism"] == "dp2" and c4["value"] > 0
     assert abs(c4["value"] - 2 * 1 * 8192 * 2 / (c4["ms_per_step"] * 1e-3 * 2)) <= 1e-3 * c4["value"]
     assert "config5_upsampler_decode" not in out  # rank 0 at N = 1 only
+
+
+@pytest.mark.timeout(600)
+def test_bench_py_bare_gpus2_spawns_ranks(cuda):
+    """`python bench.py --gpus 2` with NO outer launcher (the form the driver's BENCH command takes): bench.py starts
+    the two ranks itself as a child torch.distributed.run and waits for it. Under VQA_DIST_BACKEND=gloo both ranks
+    share the one GPU. Exactly one JSON line, n_gpus 2 / dp2 — never a silent one-GPU measurement."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(VQA_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior", "--no-roofline"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    want = 2 * 2 * 8192 / (out["ms_per_step"] * 1e-3)
+    assert abs(out["value"] - want) <= 1e-3 * want
+    assert out["config"]["exchange"] == "one bucket after the join"

@@ -141,13 +141,19 @@ class _Rccl:
         pg = group if group is not None else dist.distributed_c10d._get_default_group()
         be = pg._get_backend(device)
         if not be._comm_ptr():  # communicator created lazily (no device_id at init): one collective creates it
+            if torch.cuda.is_current_stream_capturing():
+                # a torch-managed collective inside a capture is what the watchdog aborts on (module docstring):
+                # build this object before capturing (VQVAE.capture_train_step does)
+                raise RuntimeError("vqa_dp: the RCCL communicator does not exist yet and cannot be created while "
+                                   "a graph is being captured; call vqa_dp.rccl_direct(group, device) first")
             t = torch.zeros(1, device=device)
             dist.all_reduce(t, group=group)
             torch.cuda.synchronize(device)
+        self.be = be  # held: the cache key is this object's identity, which must not be reused while cached
         self.comm = ctypes.c_void_p(be._comm_ptr())
         if not self.comm.value:
             raise RuntimeError("vqa_dp: the process group has no RCCL communicator")
-        lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))  # torch's own copy
+        lib = ctypes.CDLL(loaded_rccl_path())  # the copy torch itself loaded (its communicator lives there)
         self.all_reduce = lib.ncclAllReduce
         self.all_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_void_p, ctypes.c_void_p]
@@ -155,6 +161,14 @@ class _Rccl:
         self.err = lib.ncclGetErrorString
         self.err.argtypes, self.err.restype = [ctypes.c_int], ctypes.c_char_p
         self.log: List[int] = []  # element counts of the collectives issued (tests)
+
+    def current(self) -> bool:
+        """Is the cached communicator still the backend's live one? (A destroyed and re-created group, or a
+        backend that re-created its communicator, gives another pointer: the entry is rebuilt, never reused.)"""
+        try:
+            return self.be._comm_ptr() == self.comm.value
+        except Exception:
+            return False
 
     def run(self, bucket: torch.Tensor, regions: Sequence[Tuple[int, int]]):
         assert bucket.dtype == torch.float32 and bucket.is_contiguous()
@@ -171,14 +185,41 @@ class _Rccl:
             self.log.append(b - a)
 
 
+def loaded_rccl_path() -> str:
+    """Path of the librccl this process has already mapped (torch's own, or a system RCCL torch links against):
+    handing a communicator to a second RCCL instance would be undefined, so no other copy is ever opened."""
+    found = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6 and os.path.basename(parts[5].strip()).startswith("librccl.so"):
+                    found.append(parts[5].strip())
+    except OSError:
+        pass
+    if not found:
+        raise RuntimeError("vqa_dp: no librccl is mapped in this process (is the process group's backend RCCL?)")
+    return found[0]
+
+
 _RCCL: Dict[Tuple[int, str], _Rccl] = {}
 
 
 def rccl_direct(group, device: torch.device) -> _Rccl:
-    key = (id(group), str(device))
-    if key not in _RCCL:
-        _RCCL[key] = _Rccl(group, device)
-    return _RCCL[key]
+    """The direct-RCCL issuer of `group` on `device`, keyed on the identity of the group's backend object and
+    checked against its live communicator pointer at every call (see `_Rccl.current`)."""
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    be = pg._get_backend(device)
+    key = (id(be), str(device))
+    ent = _RCCL.get(key)
+    if ent is None or ent.be is not be or not ent.current():
+        ent = _RCCL[key] = _Rccl(group, device)
+    return ent
+
+
+def reset():
+    """Forget every cached communicator (call before `dist.destroy_process_group()`)."""
+    _RCCL.clear()
 
 
 def exchange_regions(bucket: torch.Tensor, regions: Sequence[Tuple[int, int]], group=None) -> int:

@@ -186,7 +186,7 @@ def ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr())
 
 
-# Test hook (tests/test_gpu_race.py, tools/cotenant.py): a callable run right before every libvqa launch is
+# Test hook (tests/test_gpu_race.py, tools/cotenant.py inject): a callable run right before every libvqa launch is
 # queued, on the launching thread with the launch's stream current — the race tests use it to put random spin
 # delays in front of launches, so every cross-stream ordering the step relies on is exercised. None in the product.
 launch_hook = None

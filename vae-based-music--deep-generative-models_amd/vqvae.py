@@ -446,6 +446,9 @@ class VQVAE:
                 self._update(True)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
+        if self.overlap_exchange and vqa_dp.active(self.process_group) and vqa_dp.device_side(self.process_group):
+            # the direct-RCCL issuer (and, if the group made it lazily, its communicator) exists before the capture
+            vqa_dp.rccl_direct(self.process_group, self.device)
         self._graph_pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=self._graph_pool, capture_error_mode="thread_local"):
@@ -461,12 +464,19 @@ class VQVAE:
             with torch.cuda.graph(g2, pool=self._graph_pool, capture_error_mode="thread_local"):
                 self._update(True)
         self._graph = (g1, g2)
+        # the exchange form the graphs were captured around, fixed here: an eager step in between (test_step,
+        # evaluate) rewrites self._overlapped with ITS form
+        self._graph_overlapped = self._overlapped
         torch.cuda.synchronize(self.device)
 
     def _replay(self):
         g1, g2 = self._graph
+        self._overlapped = self._graph_overlapped
         g1.replay()
         if g2 is not None:
+            # split graphs: the whole bucket is exchanged between them (the per-level collectives are captured only
+            # in the one-graph form)
+            assert not self._graph_overlapped
             self._exchange()
             g2.replay()
 
