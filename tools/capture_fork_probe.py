@@ -3,7 +3,9 @@
 origin -> 3 "level" streams (work, then the level's collective, then more work) -> joined into the origin, captured
 and replayed. Patterns: the collective on one shared exchange stream forked from each level stream in turn
 (temporary events / events kept alive to capture_end), on the level stream itself, or on a per-level stream.
-    python tools/capture_fork_probe.py level|perlevel|keep|shared      (MASTER_ADDR / MASTER_PORT set)
+    python tools/capture_fork_probe.py level|perlevel|keep|shared[_torch]      (MASTER_ADDR / MASTER_PORT set)
+A `_torch` suffix replaces the ncclAllReduce on the side stream by a plain torch kernel (x.add_(0)): the same fork /
+join shape with no RCCL call inside the capture (round-6 verdict item 5).
 Measured (round 5, PyTorch 2.10 / ROCm 7.0 / RCCL 2.26.6): "level" captures and replays right; "perlevel", "keep"
 and "shared" segfault in capture_end (profiles/r5_dp_overlap.txt).
 """
@@ -38,18 +40,28 @@ def main():
         keep.append(e)
         return e
 
+    torch_op = pat.endswith("_torch")
+    base = pat[:-len("_torch")] if torch_op else pat
+
+    def launch(x, stream):
+        if torch_op:
+            with torch.cuda.stream(stream):
+                x.add_(0)
+            return 0
+        return r.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), 7, 0, r.comm, stream.cuda_stream)
+
     def coll(l):
         x, cur = xs[l], torch.cuda.current_stream()
-        if pat == "level":
-            rc = r.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), 7, 0, r.comm, cur.cuda_stream)
+        if base == "level":
+            rc = launch(x, cur)
         else:
-            side = per[l] if pat == "perlevel" else shared
-            if pat == "keep":
+            side = per[l] if base == "perlevel" else shared
+            if base == "keep":
                 side.wait_event(ev(cur))
             else:
                 side.wait_stream(cur)
-            rc = r.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), 7, 0, r.comm, side.cuda_stream)
-            if pat == "keep":
+            rc = launch(x, side)
+            if base == "keep":
                 cur.wait_event(ev(side))
             else:
                 cur.wait_stream(side)
