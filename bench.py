@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--prior-steps", type=int, default=10)
     p.add_argument("--decode-samples", type=int, default=16)
     p.add_argument("--decode-len", type=int, default=1024)
+    p.add_argument("--no-fp32", action="store_true", help="skip the fp32 config-2 leg")
+    p.add_argument("--fp32-steps", type=int, default=5)
     return p.parse_args()
 
 
@@ -163,6 +165,41 @@ def cpu_baseline(batch, steps, seq):
             "cores_note": "the GPU box gives one GPU's job a CPU share of 16 threads and sets OMP_NUM_THREADS=16 to "
                           "say so (its rules: leave that setting and size thread pools to the share); every CPU of "
                           "the affinity mask is used where no such share is set"}
+
+
+def fp32_leg(a, dev, world, batches):
+    """Config 2 at the reference's own arithmetic precision (fp32 activations, the exact fp32 MFMA path), beside the
+    bf16 headline: the same architecture, batch, chunk length, graph replay and clock as the main line (an extra key;
+    `value` stays bf16 config 2, the dtype BASELINE.json names)."""
+    from vqvae import VQVAE
+    m = VQVAE((a.seq, 1), dtype="fp32", device=dev, **CFG2)
+    m.compile()
+    m.capture_train_step(batches[0], warmup=1)
+    m.train_step(batches[1])
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.fp32_steps):
+        m.train_step(batches[i % len(batches)])
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    v = a.batch * a.seq * a.fp32_steps * world / el
+    out = {"metric": METRIC + " (fp32)", "value": round(v, 1), "value_per_gpu": round(v / world, 1),
+           "unit": "audio-samples/s", "n_gpus": world, "steps": a.fp32_steps,
+           "ms_per_step": round(el / a.fp32_steps * 1e3, 3), "dtype": "fp32",
+           "config": {"workload": "BASELINE config 2 in fp32 (the reference's arithmetic)", "global_batch": a.batch * world,
+                      "seq_len": a.seq, "graph": True},
+           "final_loss": round(float(m.results()["loss"]), 5)}
+    del m
+    torch.cuda.empty_cache()
+    return out
 
 
 def prior_legs(a, dev, world, rank):
@@ -373,6 +410,11 @@ def main():
                         "busy_frac_pmc": pmc.get("mfma_busy_frac")}
 
     legs = {}
+    if not a.no_fp32 and a.dtype == "bf16":
+        try:
+            legs["config2_fp32"] = fp32_leg(a, dev, world, batches)
+        except Exception as e:  # an extra leg must never cost the config-2 line
+            legs["config2_fp32"] = {"error": f"{type(e).__name__}: {e}"[:400]}
     if not a.no_prior:
         try:
             legs = prior_legs(a, dev, world, rank)

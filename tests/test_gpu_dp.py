@@ -428,6 +428,9 @@ def test_bench_py_dp2_gloo_one_gpu(cuda):
     assert c4["n_gpus"] == 2 and c4["config"]["parallelism"] == "dp2" and c4["value"] > 0
     assert abs(c4["value"] - 2 * 1 * 8192 * 2 / (c4["ms_per_step"] * 1e-3 * 2)) <= 1e-3 * c4["value"]
     assert "config5_upsampler_decode" not in out  # rank 0 at N = 1 only
+    # the fp32 config-2 leg through the same DP branch
+    f = out["config2_fp32"]
+    assert f["n_gpus"] == 2 and f["dtype"] == "fp32" and f["value"] > 0 and f["config"]["global_batch"] == 4
 
 
 @pytest.mark.timeout(600)
@@ -438,7 +441,7 @@ def test_bench_py_bare_gpus2_spawns_ranks(cuda):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env.update(VQA_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-           "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior", "--no-roofline"]
+           "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior --no-fp32", "--no-roofline"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

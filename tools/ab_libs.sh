@@ -10,7 +10,7 @@ mkdir -p gpurun_out/ab
 for r in $(seq $ROUNDS); do
   for v in gpurun_out/libvqa_base.so "$@"; do
     cp "$v" $LIB
-    out=$(timeout -k 10 240 python bench.py --no-cpu-baseline --no-roofline --no-prior --steps 40 --warmup 5 2>gpurun_out/ab/err.log) || { echo "bench failed for $v"; cp gpurun_out/libvqa_base.so $LIB; exit 1; }
+    out=$(timeout -k 10 240 python bench.py --no-cpu-baseline --no-roofline --no-prior --no-fp32 --steps 40 --warmup 5 2>gpurun_out/ab/err.log) || { echo "bench failed for $v"; cp gpurun_out/libvqa_base.so $LIB; exit 1; }
     echo "$(basename $v) $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["ms_per_step"])')"
   done
 done

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 ROUNDS=$1; shift
 for r in $(seq 1 $ROUNDS); do
   for e in "$@"; do
-    ms=$(env $e timeout -k 10 300 python bench.py --no-cpu-baseline --no-prior --no-roofline --steps 30 2>/dev/null | python -c "import json,sys; print(json.loads(sys.stdin.read().strip().splitlines()[-1])['ms_per_step'])")
+    ms=$(env $e timeout -k 10 300 python bench.py --no-cpu-baseline --no-prior --no-fp32 --no-roofline --steps 30 2>/dev/null | python -c "import json,sys; print(json.loads(sys.stdin.read().strip().splitlines()[-1])['ms_per_step'])")
     echo "round $r [${e:-default}] $ms ms/step"
   done
 done

@@ -3,6 +3,10 @@
 #   entry              the round's new GPU tests (bare bench --gpus 2, replay after test_step, random-delay race),
 #                      the RCCL world-size-1 tests, then ONE capture probe form (argument; may segfault: last step)
 #   probe FORM         tools/capture_fork_probe.py FORM alone (world size 1)
+#   rsab LIB...        residual-block builds: outputs bitwise vs variants/libvqa_r5.so (tools/rs_bitwise.py),
+#                      tests/test_gpu_resblock.py, per-launch sweep (r5 and each build), step A/B (in-tree vs builds)
+#   stamps LIB...      per-phase s_memtime stamps (libraries built with -DVQA_RS_STAMPS): backward d = 1, 9, 27 and
+#                      the forward, T = 32768
 #   close TAG          full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
 NAME=$1; shift
@@ -25,6 +29,32 @@ entry)
   [ -n "$1" ] && probe "$1" ;;
 probe)
   probe "$1" ;;
+rsab)
+  VQA_LIB_PATH=variants/libvqa_r5.so timeout -k 10 300 python -u tools/rs_bitwise.py --save $OUT/ref.pt 2>&1 \
+    | grep -v amdgpu.ids || exit 1
+  for v in "$@"; do
+    echo "== bitwise $v"
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/rs_bitwise.py --check $OUT/ref.pt 2>&1 | grep -v amdgpu.ids | tail -40
+    [ ${PIPESTATUS[0]} -le 1 ] || exit 1
+  done
+  rm -f $OUT/ref.pt
+  for v in "$@"; do
+    VQA_LIB_PATH=$v timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+      tests/test_gpu_resblock.py > $OUT/t_$(basename $v).log 2>&1 || { tail -30 $OUT/t_$(basename $v).log; exit 1; }
+    echo "tests $v: $(tail -1 $OUT/t_$(basename $v).log)"
+  done
+  for v in variants/libvqa_r5.so "$@"; do
+    echo "== sweep $v"
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/resblock_sweep.py --T 32768 8192 2048 512 --reps 10 --fused-only 2>&1 \
+      | grep -v amdgpu.ids || exit 1
+  done
+  bash tools/ab_libs.sh 3 variants/libvqa_r5.so "$@" ;;
+stamps)
+  for v in "$@"; do
+    echo "== stamps $v"
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/rs_stamps.py --T 32768 --d 1 9 27 2>&1 | grep -v amdgpu.ids || exit 1
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/rs_stamps.py --T 32768 --d 1 9 27 --fwd 2>&1 | grep -v amdgpu.ids || exit 1
+  done ;;
 close)
   TAG=$1
   timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \

@@ -37,6 +37,7 @@ def main():
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--T", type=int, nargs="*", default=[32768, 16384, 8192, 2048])
+    p.add_argument("--fused-only", action="store_true", help="skip the unfused two-conv timings")
     a = p.parse_args()
     import vqa_lib as V
     dev = torch.device("cuda", 0)
@@ -65,6 +66,10 @@ def main():
                                          V.BF16, dfr)
                 V.conv1d_bwd_data_weight(dh, wa, x, dy, dx, gw[0], gw[1], B, T, T, C, C, 3, 1, d, d,
                                          V.PRE_RELU | V.ADD_RESIDUAL, V.BF16, dfr)
+            if a.fused_only:
+                print(f"T={T:6d} d={d:2d}  fused fwd {f_us:7.1f} us ({2 * unit / f_us / 1e3:5.0f} GB/s)  "
+                      f"bwd {b_us:7.1f} us ({3 * unit / b_us / 1e3:5.0f} GB/s)", flush=True)
+                continue
             uf_us = timed(unf_f, a.reps)
             ub_us = timed(unf_b, a.reps)
             dfr.descs, dfr.keep = [], []

@@ -19,7 +19,7 @@ if [ $rc -ne 0 ]; then echo "tests failed ($rc)"; exit $rc; fi
 for lib in base variant; do
   if [ $lib = variant ]; then cp "$V" $L; fi
   VQA_LEVEL_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$lib -o t -- \
-    python bench.py --no-cpu-baseline --no-roofline --no-prior --steps 10 > $OUT/bench_serial_$lib.json 2>$OUT/err_$lib || { cp $OUT/base.so $L; echo "trace failed"; exit 1; }
+    python bench.py --no-cpu-baseline --no-roofline --no-prior --no-fp32 --steps 10 > $OUT/bench_serial_$lib.json 2>$OUT/err_$lib || { cp $OUT/base.so $L; echo "trace failed"; exit 1; }
   python tools/step_breakdown.py $OUT/trace_$lib/t_kernel_trace.csv > $OUT/breakdown_$lib.txt
   find $OUT/trace_$lib -name "*kernel_trace.csv" -size +20M -delete
 done

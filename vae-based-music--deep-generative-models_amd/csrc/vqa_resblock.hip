@@ -550,9 +550,11 @@ void resblock_fwd_kernel(ResArgs a) {
 //   team H (2, 3)  dh = conv_b^T(dy) * (h > 0) -> D (its own buffer);                then dW_a from X, D
 // Barriers per tile: H ready, D ready, every read done (then the next tile's staged rows are stored), the
 // stored rows visible: four (the one-buffer form needs five).
-// HALVES = 2: a 512-thread workgroup whose two 4-wave halves run the same pipeline on their own tiles (even / odd
-// offsets of the workgroup's range, each half its own LDS region) and add their weight gradients through LDS at the
-// end in a fixed order: ONE partial row per two tile streams (half the partial-row bytes of two workgroups)
+// HALVES = 2 (not instantiated; measured 4 % slower on the step): a 512-thread workgroup whose two
+// 4-wave halves run the same pipeline on their own tiles (even / odd offsets of the workgroup's range, each half its
+// own LDS region) and add their weight gradients through LDS at the end in a fixed order. The product launches
+// HALVES = 1, whose code the half logic compiles out of. (The LDS-DMA staged form measured in round 5 is in git
+// history at 8432c5f.)
 template <class T, int DT, int RT = rs_bwd_rt(DT), int HALVES = 1>
 __global__ __launch_bounds__(256 * HALVES) void resblock_bwd_kernel(ResArgs a) {
   typedef Mfma<T> M;
@@ -744,14 +746,12 @@ __global__ __launch_bounds__(256 * HALVES) void resblock_bwd_kernel(ResArgs a) {
     RS_STAMP(3);
     __syncthreads();
     RS_STAMP(4);
-#ifndef VQA_RS_LATE_WAIT
     // The next tile's staged rows (loaded a tile ago) are waited for HERE, before this tile's dx stores are issued.
     // vmcnt counts loads and stores in one queue: left to the compiler, the wait sits at the rows' register use at the
     // end of the tile — after team W's dx stores — and, its count merged over both teams' paths, also waits for
     // those stores' write acknowledgements (s_waitcnt vmcnt(0) there; every wave then idles at the next barrier).
     // A real s_waitcnt here (the builtin: the compiler's wait pass accounts for it) leaves the later use waitless.
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
-#endif
     RS_STAMP(5);
     // 3. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows, NJB n-tiles nt(j) at a time (nt(j) >= NT: none)
     const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
@@ -845,329 +845,6 @@ __global__ __launch_bounds__(256 * HALVES) void resblock_bwd_kernel(ResArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Backward with LDS-DMA staging and double-buffered x / dy tiles (bf16; the model's dilations 1, 3, 9, 27).
-// The same teams and products as resblock_bwd_kernel, but the x and dy rows go HBM -> LDS by
-// buffer_load_dwordx4 ... lds (no VGPR round trip, no ds_write pass, no staging registers) into one of two
-// buffer sets: tile i+1's rows land while tile i is computed, and a tile ends with ONE barrier where the
-// register-staged form needs two (wait for every read of the tile, store the staged rows, publish them).
-//   tile start     issue the next tile's DMA into the other set
-//   all waves      h = relu(conv_a(relu x))  -> H                         barrier
-//   team W / H     dW_b from H, dy  /  dh = conv_b^T(dy) * (h > 0) -> D   barrier
-//   team W / H     dx -> HBM        /  dW_a from relu(x), D;  each wave waits for its own DMA, barrier
-// x stays raw in LDS (relu applied to the fragments that need it; the x > 0 mask reads it directly).
-// An LDS-DMA instruction writes 64 lanes x 16 B contiguously (1 KiB = 16 rows of 64 B), so these buffers have
-// unpadded 64-byte rows; bank conflicts are removed by the layout of each 16-row block instead (every lane's
-// SOURCE address picks the row / chunk its slot receives): logical row r = 4s + u (s = (r >> 2) & 3), 16-byte
-// chunk c  ->  byte 64 (r & ~3) + 64 (u ^ (c & 1)) + 16 (c ^ s). ds_read_b128 fragment reads (8 rows of each
-// parity, chunk pairs {0, 2} / {1, 3} per lane group) and ds_read_b64_tr_b16 reads (8 rows of one parity, two
-// adjacent chunks) then touch 16 distinct 16-byte bank slots per group, for any first row (tools/lds_banks.py).
-// relu(h) and dh keep the padded 80-byte rows of the register-staged kernel (they are written by ds_write).
-// bf16 backward of the compiled dilations through the LDS-DMA kernel (resblock_bwd_dma_kernel)
-#ifndef VQA_RS_DMA
-#define VQA_RS_DMA 0
-#endif
-constexpr bool kRsDma = VQA_RS_DMA;
-#ifndef VQA_RS_DMA_MODE
-#define VQA_RS_DMA_MODE 1
-#endif
-constexpr int kRsDmaMode = VQA_RS_DMA_MODE;  // who issues the next tile's DMA: 0 every wave at tile start, 1 team W after dW_b
-#ifndef VQA_RS_DMA_D27
-#define VQA_RS_DMA_D27 0
-#endif
-constexpr bool kRsDma27 = VQA_RS_DMA_D27;  // d = 27 at 96-row tiles (the DMA plan's LDS) against 128 register-staged
-typedef int rs_v4i __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ int sw_off(int r, int c) {
-  return ((r & ~3) << 6) + (((r & 3) ^ (c & 1)) << 6) + ((c ^ ((r >> 2) & 3)) << 4);
-}
-
-// buffer descriptor as 4 SGPRs (inline-asm operand): raw, num_records = bytes (rows outside the item read 0)
-__device__ __forceinline__ rs_v4i rs_rsrc4(const void* base, unsigned bytes) {
-  const unsigned long long p = (unsigned long long)base;
-  return rs_v4i{(int)__builtin_amdgcn_readfirstlane((unsigned)p), (int)__builtin_amdgcn_readfirstlane((unsigned)(p >> 32)),
-                (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000};
-}
-
-// one 16-row block: lane l's 16 bytes (its own source offset) -> LDS lds + 16 l (M0 = the block's LDS byte address).
-// Inline asm, so the compiler's wait bookkeeping does not see it (the builtin form makes every later LDS read of
-// the one LDS array wait vmcnt(0)); the kernel counts its completion itself (rs_wait_vm) before the publishing barrier.
-__device__ __forceinline__ void rs_dma16(rs_v4i rsrc, unsigned voff, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
-// s_waitcnt vmcnt(N) (expcnt / lgkmcnt not waited)
-template <int N> __device__ __forceinline__ void rs_wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-// bf16 fragment (8 K values down 32 rows) from the DMA layout: rows r0 + trr (+16), the lane's 8-byte piece of
-// 16-byte chunk c (ds_read_b64_tr_b16 x 2, the lane map of rs_rows)
-__device__ __forceinline__ bf16x8 sw_rows(const char* buf, int r16, int m, int c) {
-  typedef short v4s __attribute__((ext_vector_type(4)));
-  typedef short v8s __attribute__((ext_vector_type(8)));
-  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const int trr = 2 * (4 * (g & 1) + (i >> 2)) + (g >> 1);
-  const char* p = buf + 64 * r16 + sw_off(m + trr, c + ((i & 3) >> 1)) + 8 * (i & 1);
-  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
-  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p + 1024));
-  return __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-// conv over a DMA-layout buffer, NJ n-tiles: B fragment of n-tile j, tap k = logical rows r16[j] + OFF + k TAP + pi(lane)
-// (r16[j] a multiple of 16), K order and accumulation order of conv_multi<bf16, RELU_IN, KPERM = true>
-template <bool RELU_IN, int NJ, int OFF, int TAP, class AFrag>
-__device__ __forceinline__ void conv_sw(f32x4 (&acc)[NJ][2], AFrag afrag, const char* buf, const int (&r16)[NJ],
-                                        f32x4 init0 = f32x4{0.f, 0.f, 0.f, 0.f},
-                                        f32x4 init1 = f32x4{0.f, 0.f, 0.f, 0.f}) {
-  const int lane = threadIdx.x & 63, pn = rs_pi(lane & 15), c = rs_ocol(lane) >> 3;
-  bf16x8 b[NJ][3];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int off = OFF + k * TAP;  // >= 0, compile-time after unrolling
-      b[j][k] = *(const bf16x8*)(buf + 64 * (r16[j] + (off & ~15)) + sw_off((off & 15) + pn, c));
-      if (RELU_IN) b[j][k] = relu_frag(b[j][k]);
-    }
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    acc[j][0] = init0;
-    acc[j][1] = init1;
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      acc[j][0] = Mfma<bf16>::mma(afrag(k, 0, 0), b[j][k], acc[j][0]);
-      acc[j][1] = Mfma<bf16>::mma(afrag(k, 1, 0), b[j][k], acc[j][1]);
-    }
-  __builtin_amdgcn_sched_group_barrier(0x100, NJ * 3, 0);
-  __builtin_amdgcn_sched_group_barrier(0x008, NJ * 6, 0);
-}
-
-// rows per tile of the DMA kernel: two x / dy sets + relu(h) + dh within 80 KiB (two workgroups per CU)
-constexpr int rs_dma_rt(int d) { return d <= 3 ? 160 : d <= 9 ? 128 : 96; }
-constexpr int rs_dma_setb(int d, int rt) {
-  return ((round16(rt + 2 * d) + 2 * d + 15) / 16 + (round16(rt + 2 * d) + 2 + 15) / 16) * 1024;
-}
-static size_t bwd_dma_lds(int d) {
-  const int rt = rs_dma_rt(d), HR = round16(rt + 2 * d);
-  return (size_t)2 * rs_dma_setb(d, rt) + (size_t)2 * HR * rs_stride<bf16>() * 2;
-}
-
-template <int DT, int RT = rs_dma_rt(DT)>
-__global__ __launch_bounds__(256) void resblock_bwd_dma_kernel(ResArgs a) {
-  typedef bf16 T;
-  typedef Mfma<T> M;
-  constexpr int d = DT, XS = rs_stride<T>(), NT = RT / 16;
-  constexpr int HR = round16(RT + 2 * d), XR = HR + 2 * d, YR = HR + 2;
-  constexpr int NXB = (XR + 15) / 16, NYB = (YR + 15) / 16, NB = NXB + NYB, SETB = NB * 1024;
-  static_assert(SETB == rs_dma_setb(DT, RT), "LDS plan");
-  constexpr int NHT = HR / 16, NP1 = (NHT + 3) / 4, P1A = NP1 < 3 ? NP1 : 3, P1B = NP1 - P1A;
-  constexpr int NDH = (NHT + 1) / 2, DH1 = NDH < 3 ? NDH : 3, DH2 = NDH - DH1 < 3 ? NDH - DH1 : 3,
-                DH3 = NDH - DH1 - DH2;
-  constexpr int NA = NT / 2, NA1 = NA < 3 ? NA : 3, NA2 = NA - NA1;
-  static_assert(NT % 2 == 0 && NA2 <= 3 && P1B <= 3 && DH3 <= 3, "tile plan");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* H = (T*)(smem + 2 * SETB);  // local i <-> row t0 - d + i: relu(h)
-  T* D = H + HR * XS;             // local i <-> row t0 - d + i: dh
-  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int team = wave >> 1, tw = wave & 1;
-  const int tbeg = blockIdx.x * a.tpw + min((int)blockIdx.x, a.textra),
-            tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
-  if (tbeg >= tend) return;
-  // the 16-byte slot of lane l in a 16-row block <- logical (row 4s + u, chunk c) of the layout above
-  const int ds = lane >> 4, dc = (lane & 3) ^ ds, du = ((lane >> 2) & 3) ^ (dc & 1);
-  const int dma_lane = (4 * ds + du) * 64 + 16 * dc;
-  const unsigned ibytes = (unsigned)a.T * RC * (unsigned)sizeof(T);
-  // x rows t0 - 2d + j (set + j), dy rows t0 - d - 1 + m (set + NXB blocks + m): blocks wave, wave + 4, ...
-  // blocks w, w + NWV, ... of the NWV issuing waves (w = the wave's index among them)
-  auto dma_tile = [&](auto nwv, int w, int set, const RsCursor& c) {
-    constexpr int NWV = decltype(nwv)::value;
-    const size_t o = (size_t)c.n * a.T * RC;
-    const rs_v4i rx = rs_rsrc4((const T*)a.x + o, ibytes), ry = rs_rsrc4((const T*)a.dy + o, ibytes);
-    const int r0 = c.tm * RT;
-    const unsigned sb = lds0 + set * SETB;
-#pragma unroll
-    for (int t = 0; t < (NB + NWV - 1) / NWV; ++t) {
-      const int blk = w + NWV * t;  // wave-uniform: scalar selects, one branch for the last partial round
-      const bool isx = blk < NXB;
-      const rs_v4i r = isx ? rx : ry;
-      const int row = isx ? r0 + 16 * blk - 2 * d : r0 + 16 * (blk - NXB) - d - 1;
-      if (NWV * t + NWV - 1 < NB || blk < NB) rs_dma16(r, (unsigned)(row * 64 + dma_lane), sb + blk * 1024);
-    }
-  };
-  RsCursor cur, ldc;
-  cur.set(tbeg, a.ntm);
-  ldc = cur;
-  dma_tile(std::integral_constant<int, 4>{}, wave, 0, ldc);
-  typename M::frag wfa[3][2][1], wt[3][2][1];
-  load_wfrags<T, true>(wfa, a.wa);
-  load_wfrags_t<T>(wt, team == 0 ? a.wa : a.wb);
-  const int pn = rs_pi(lane & 15), oc = rs_ocol(lane), cb = oc >> 3;
-  f32x4 bav[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) bav[mt] = a.ba ? bias4(a.ba, oc + 4 * mt) : f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 gw[2][3], gb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gw[o][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto wa_frag = [&](int k, int mt, int) { return wfa[k][mt][0]; };
-  auto wt_frag = [&](int k, int mt, int) { return wt[k][mt][0]; };
-  rs_wait_vm<0>();
-  __syncthreads();
-  for (int tile = tbeg; tile < tend; ++tile, cur.next(a.ntm)) {
-    const int n = cur.n, t0 = cur.tm * RT, set = (tile - tbeg) & 1;
-#ifdef VQA_RS_STAMPS
-    const bool stamp_on = tile == tbeg + 4;
-#endif
-    RS_STAMP(0);
-    const char* X = smem + set * SETB;
-    const char* Y = X + NXB * 1024;
-    const bool more = tile + 1 < tend;
-    if (more) ldc.next(a.ntm);
-    if (kRsDmaMode == 0 && more) dma_tile(std::integral_constant<int, 4>{}, wave, set ^ 1, ldc);
-    const bool interior = t0 - d >= 0 && t0 - d + HR <= a.T;  // uniform: no SAME-padding rows
-    // 1. relu(h) over the dh rows (zero outside the item): n-tiles wave + 4 (j0 + j)
-    auto h_batch = [&](auto nj, int j0) {
-      constexpr int NJB = decltype(nj)::value;
-      int rh[NJB];
-#pragma unroll
-      for (int j = 0; j < NJB; ++j) rh[j] = min(wave + 4 * (j0 + j), NHT - 1) * 16;
-      f32x4 acc[NJB][2];
-      conv_sw<true, NJB, 0, d>(acc, wa_frag, X, rh, bav[0], bav[1]);
-      auto store_h = [&](auto edge) {
-#pragma unroll
-        for (int j = 0; j < NJB; ++j) {
-          if (wave + 4 * (j0 + j) >= NHT) continue;
-          const int i = rh[j] + pn;
-          uint4 u = __builtin_bit_cast(uint4, relu_frag(__builtin_bit_cast(bf16x8, bf16_bits(acc[j][0], acc[j][1]))));
-          if constexpr (decltype(edge)::value) {
-            const int r = t0 - d + i;
-            if (r < 0 || r >= a.T) u = uint4{0u, 0u, 0u, 0u};
-          }
-          *(uint4*)(H + i * XS + oc) = u;
-        }
-      };
-      if (interior) store_h(std::false_type{});
-      else store_h(std::true_type{});
-    };
-    h_batch(std::integral_constant<int, P1A>{}, 0);
-    if constexpr (P1B > 0) h_batch(std::integral_constant<int, P1B>{}, P1A);
-    RS_STAMP(1);
-    __syncthreads();
-    RS_STAMP(2);
-    if (team == 0) {
-      // 2W. dW_b[k][c][o] += sum_t relu(h)[t+k-1][c] dy[t][o] (c in tile tw, every o), db_b[o in tile tw]
-      constexpr int YO = d + 1;
-#pragma unroll
-      for (int kk = 0; kk < RT; kk += 32) {
-        const bf16x8 b0 = sw_rows(Y, kk + (YO & ~15), YO & 15, 0);
-        const bf16x8 b1 = sw_rows(Y, kk + (YO & ~15), YO & 15, 2);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const bf16x8 af = rs_rows(H + (d + k - 1 + kk) * XS + tw * 16, XS);
-          gw[0][k] = M::mma(af, b0, gw[0][k]);
-          gw[1][k] = M::mma(af, b1, gw[1][k]);
-        }
-        gb = M::mma(M::ones(), tw ? b1 : b0, gb);
-      }
-      // mode 1: team W issues the next tile's DMA here, in the time it would wait for team H's dh
-      if (kRsDmaMode == 1 && more) dma_tile(std::integral_constant<int, 2>{}, tw, set ^ 1, ldc);
-    } else {
-      // 2H. dh = conv_b^T(dy) * (h > 0) -> D: n-tiles tw + 2 (j0 + j)
-      auto dh_batch = [&](auto nj, int j0) {
-        constexpr int NJB = decltype(nj)::value;
-        int rh[NJB];
-#pragma unroll
-        for (int j = 0; j < NJB; ++j) rh[j] = min(tw + 2 * (j0 + j), NHT - 1) * 16;
-        f32x4 dh[NJB][2];
-        conv_sw<false, NJB, 2, -1>(dh, wt_frag, Y, rh);
-#pragma unroll
-        for (int j = 0; j < NJB; ++j) {
-          if (tw + 2 * (j0 + j) >= NHT) continue;
-          const int i = rh[j] + pn;
-          *(uint4*)(D + i * XS + oc) = mask_pos8(bf16_bits(dh[j][0], dh[j][1]), *(const uint4*)(H + i * XS + oc));
-        }
-      };
-      dh_batch(std::integral_constant<int, DH1>{}, 0);
-      if constexpr (DH2 > 0) dh_batch(std::integral_constant<int, DH2>{}, DH1);
-      if constexpr (DH3 > 0) dh_batch(std::integral_constant<int, DH3>{}, DH1 + DH2);
-    }
-    RS_STAMP(3);
-    __syncthreads();
-    RS_STAMP(4);
-    if (team == 0) {
-      // 3W. dx = dy + conv_a^T(dh) * (x > 0) on the tile's rows, n-tiles tw, tw + 2, ...
-      const __amdgpu_buffer_rsrc_t dxr = rs_rsrc((T*)a.y + (size_t)n * a.T * RC, ibytes);
-      auto dx_batch = [&](auto nj, int j0) {
-        constexpr int NJB = decltype(nj)::value;
-        int rb[NJB];
-        f32x4 acc[NJB][2];
-#pragma unroll
-        for (int j = 0; j < NJB; ++j) rb[j] = (tw + 2 * (j0 + j)) * 16 + 2 * d;
-        conv_multi<T, false, true, false, NJB>(acc, wt_frag, D, rb, -d);
-#pragma unroll
-        for (int j = 0; j < NJB; ++j) {
-          const int r16 = (tw + 2 * (j0 + j)) * 16, tl = r16 + pn;
-          constexpr int XO = 2 * d, YO = d + 1;
-          bool xp[8];
-          f32x4 y0, y1;
-          pos8((const T*)(X + 64 * (r16 + (XO & ~15)) + sw_off((XO & 15) + pn, cb)), xp);
-          ld8((const T*)(Y + 64 * (r16 + (YO & ~15)) + sw_off((YO & 15) + pn, cb)), y0, y1);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            y0[q] += xp[q] ? acc[j][0][q] : 0.f;
-            y1[q] += xp[4 + q] ? acc[j][1][q] : 0.f;
-          }
-          st8_buf<T>(dxr, ((t0 + tl) * RC + oc) * (int)sizeof(T), y0, y1);  // rows >= T dropped
-        }
-      };
-      dx_batch(std::integral_constant<int, NA1>{}, 0);
-      if constexpr (NA2 > 0) dx_batch(std::integral_constant<int, NA2>{}, NA1);
-      rs_wait_vm<NA>();  // this wave's DMA (issued before its NA dx stores) has landed
-      RS_STAMP(5);
-    } else {
-      // 3H. dW_a[k][c][o] += sum_t relu(x)[t+(k-1)d][c] dh[t][o] (c in tile tw, every o), db_a[o in tile tw]
-#pragma unroll
-      for (int kk = 0; kk < RT; kk += 32) {
-        const bf16x8 b0 = rs_rows(D + (d + kk) * XS, XS);
-        const bf16x8 b1 = rs_rows(D + (d + kk) * XS + 16, XS);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int xo = (k + 1) * d;
-          const bf16x8 af = relu_frag(sw_rows(X, kk + (xo & ~15), xo & 15, 2 * tw));
-          gw[0][k] = M::mma(af, b0, gw[0][k]);
-          gw[1][k] = M::mma(af, b1, gw[1][k]);
-        }
-        gb = M::mma(M::ones(), tw ? b1 : b0, gb);
-      }
-      rs_wait_vm<0>();
-      RS_STAMP(5);
-    }
-    RS_STAMP(6);
-    __syncthreads();  // the next set has landed and is visible; every read of this tile's set, H and D is done
-    RS_STAMP(7);
-  }
-  // partial rows (team W: dW_b | db_b into part_b; team H: dW_a | db_a into part_a), Keras dW[k][c][o]
-  float* pr = (team == 0 ? a.part_b : a.part_a) + (size_t)blockIdx.x * (3 * RC * RC + RC);
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        pr[(k * RC + tw * 16 + 4 * (lane >> 4) + r) * RC + o * 16 + (lane & 15)] = gw[o][k][r];
-  if (lane < 16) pr[3 * RC * RC + tw * 16 + lane] = gb[0];
-}
-
-// ---------------------------------------------------------------------------------------------------
 static int rs_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -1177,10 +854,7 @@ static int rs_cus() {
   }();
   return n;
 }
-#ifndef VQA_RS_PER_CU
-#define VQA_RS_PER_CU 2
-#endif
-constexpr int kResPerCU = VQA_RS_PER_CU;  // persistent workgroups per CU (also bounds the partial rows)
+constexpr int kResPerCU = 2;  // persistent workgroups per CU (also bounds the partial rows)
 // backward: tiles per workgroup at least (bounds the partial rows of short launches). 2 against 4, 3 and 1 in
 // alternating same-box runs: 7.316 ms/step (5 runs) vs 7.363 (4), 7.355 (3), 7.369 (1): level 2's short launches
 // (T <= 4096) are latency-bound chains of tiles per workgroup
@@ -1222,10 +896,6 @@ template <class T> struct RsFwd {
 template <class T> struct RsBwd {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D>; }
 };
-// two tile streams per 512-thread workgroup (HALVES = 2): half the partial rows of the long launches
-template <class T> struct RsBwdPair {
-  template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D, rs_bwd_rt(D), 2>; }
-};
 // the 128-row tile plan of d <= 9 (shorter launches: whole rounds of tiles per workgroup, see bwd_rt_for)
 template <class T> struct RsBwd128 {
   template <int D> static const void* fn() { return (const void*)resblock_bwd_kernel<T, D, (D > 0 && D <= 9) ? 128 : rs_bwd_rt(D)>; }
@@ -1244,18 +914,11 @@ template <class F> static const void* rs_pick(int d) {
 
 static int fwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_fwd_rt(d) : RTM; }
 static int bwd_rt_of(int d) { return (d == 1 || d == 3 || d == 9 || d == 27) ? rs_bwd_rt(d) : RTM; }
-#ifndef VQA_RS_RT128_BELOW
-#define VQA_RS_RT128_BELOW 8192
-#endif
-// rows per backward tile for a launch: d <= 9 items shorter than VQA_RS_RT128_BELOW rows use 128-row tiles (whole
+// rows per backward tile for a launch: d <= 9 items shorter than 8192 rows use 128-row tiles (whole
 // 2-tile rounds per workgroup: 0.4-1.0 us faster per launch at T = 1024-4096; slower from T = 8192, where
 // 160-row tiles keep less halo per row; profiles/r5_resblock_dma.txt)
-#ifndef VQA_RS_PAIR_FROM
-#define VQA_RS_PAIR_FROM (1 << 30)
-#endif
-constexpr int kRsPairFrom = VQA_RS_PAIR_FROM;  // items of at least this many rows: RsBwdPair
 static int bwd_rt_for(int d, int T) {
-  return (d == 1 || d == 3 || d == 9) && T < VQA_RS_RT128_BELOW ? 128 : bwd_rt_of(d);
+  return (d == 1 || d == 3 || d == 9) && T < 8192 ? 128 : bwd_rt_of(d);
 }
 
 static void plan(ResArgs& a, int per_cu, int rt, int min_tiles = 1) {
@@ -1334,37 +997,19 @@ extern "C" int vqa_resblock_bwd(const void* dy, const void* x, const float* wa, 
   // larger than a tile's activations, so short launches use fewer, longer-lived workgroups
   const int esz = dtype == VQA_BF16 ? 2 : 4;
   const hipStream_t s = (hipStream_t)stream;
-  if (kRsDma && dtype == VQA_BF16 && (dilation == 1 || dilation == 3 || dilation == 9 || (kRsDma27 && dilation == 27))) {
-    plan(a, kResPerCU, rs_dma_rt(dilation), kResMinTiles);
-    a.part_b = a.part_a + (size_t)a.nwg * E;
-    const void* fn = dilation == 1   ? (const void*)resblock_bwd_dma_kernel<1>
-                     : dilation == 3 ? (const void*)resblock_bwd_dma_kernel<3>
-                     : dilation == 9 ? (const void*)resblock_bwd_dma_kernel<9>
-                                     : (const void*)resblock_bwd_dma_kernel<27>;
-    const size_t lds = bwd_dma_lds(dilation);
-    if (int rc = set_lds(fn, lds)) return rc;
-    void* args[] = {&a};
-    (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(256), args, lds, s);
-    VQA_LAUNCHED("resblock_bwd_dma_kernel");
-  } else {
-    const int rt = bwd_rt_for(dilation, T);
-    // long launches: one 512-thread workgroup per CU running two tile streams (RsBwdPair), one partial row each
-    const bool pair = dtype == VQA_BF16 && rt == bwd_rt_of(dilation) && T >= kRsPairFrom &&
-                      (dilation == 1 || dilation == 3 || dilation == 9 || dilation == 27);
-    plan(a, pair ? kResPerCU / 2 : kResPerCU, rt, pair ? 2 * kResMinTiles : kResMinTiles);
-    a.part_b = a.part_a + (size_t)a.nwg * E;
-    const size_t lds = bwd_lds(dilation, esz, rt) * (pair ? 2 : 1);
-    size_t lds_max = bwd_lds(RMAXD, esz, RTM);  // one reservation for every dilation (the largest plan)
-    for (int dd : {1, 3, 9, 27}) lds_max = std::max(lds_max, bwd_lds(dd, esz, rs_bwd_rt(dd)));
-    const void* fn = pair ? rs_pick<RsBwdPair<bf16>>(dilation)
-                     : rt != bwd_rt_of(dilation)
-                         ? (dtype == VQA_BF16 ? rs_pick<RsBwd128<bf16>>(dilation) : rs_pick<RsBwd128<float>>(dilation))
-                         : (dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation));
-    if (int rc = set_lds(fn, pair ? 2 * lds_max : lds_max)) return rc;
-    void* args[] = {&a};
-    (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(pair ? 512 : 256), args, lds, s);
-    VQA_LAUNCHED("resblock_bwd_kernel");
-  }
+  const int rt = bwd_rt_for(dilation, T);
+  plan(a, kResPerCU, rt, kResMinTiles);
+  a.part_b = a.part_a + (size_t)a.nwg * E;
+  const size_t lds = bwd_lds(dilation, esz, rt);
+  size_t lds_max = bwd_lds(RMAXD, esz, RTM);  // one reservation for every dilation (the largest plan)
+  for (int dd : {1, 3, 9, 27}) lds_max = std::max(lds_max, bwd_lds(dd, esz, rs_bwd_rt(dd)));
+  const void* fn = rt != bwd_rt_of(dilation)
+                       ? (dtype == VQA_BF16 ? rs_pick<RsBwd128<bf16>>(dilation) : rs_pick<RsBwd128<float>>(dilation))
+                       : (dtype == VQA_BF16 ? rs_pick<RsBwd<bf16>>(dilation) : rs_pick<RsBwd<float>>(dilation));
+  if (int rc = set_lds(fn, lds_max)) return rc;
+  void* args[] = {&a};
+  (void)hipLaunchKernel(fn, dim3(a.nwg), dim3(256), args, lds, s);
+  VQA_LAUNCHED("resblock_bwd_kernel");
   const int nwg = a.nwg;
   const vqa_partials_desc da{a.part_a, dwa, dba, nwg, E, 3 * RC * RC, 0};
   const vqa_partials_desc dbd{a.part_b, dwb, dbb, nwg, E, 3 * RC * RC, 0};
