@@ -417,9 +417,9 @@ def main():
             legs["config2_fp32"] = {"error": f"{type(e).__name__}: {e}"[:400]}
     if not a.no_prior:
         try:
-            legs = prior_legs(a, dev, world, rank)
+            legs.update(prior_legs(a, dev, world, rank))
         except Exception as e:  # an extra leg must never cost the config-2 line
-            legs = {"prior_legs_error": f"{type(e).__name__}: {e}"[:400]}
+            legs["prior_legs_error"] = f"{type(e).__name__}: {e}"[:400]
 
     out = None
     if rank == 0:

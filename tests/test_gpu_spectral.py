@@ -145,3 +145,25 @@ def test_gradient_overlap_add_forms(cuda, args):
     assert abs(float(out) - float(per.mean())) / float(per.mean()) < 1e-5
     err = (dr.cpu().double() - g_ref).abs().max() / g_ref.abs().max()
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("B,T", [(3, 4096 + 113), (1, 1200), (2, 8192 + 1)])
+def test_pair_magnitudes_vs_oracle(cuda, B, T):
+    """The target spectrograms as vqa_spectral_target writes them (the frame-pair kernel in its magnitude mode, both
+    frames of a pair from one complex FFT; an odd frame count leaves the last frame unpaired), read out of the
+    target buffer by its layout (per resolution: twiddles 2N | window | |S_x| (B*F, N/2 + 1), each 64-float
+    aligned), against the oracle's |tf.signal.stft| at 2e-6 of the spectrum's max."""
+    x, _ = _signals(B, T, seed=5 + T)
+    tgt = SpectralTarget(x.to(cuda))
+    buf = tgt.mags.view(torch.float32).cpu() if tgt.mags.dtype != torch.float32 else tgt.mags.cpu()
+    al = lambda n: (n + 63) // 64 * 64  # noqa: E731
+    o = 0
+    for n_fft, hop, win in RES:
+        F = 1 + (T - win) // hop
+        o += al(2 * n_fft) + al(win)
+        got = buf[o:o + B * F * (n_fft // 2 + 1)].double().reshape(B, F, n_fft // 2 + 1)
+        o += al(B * F * (n_fft // 2 + 1))
+        ref = R.spectral(x.squeeze(-1).double(), n_fft, hop, win)
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        err = (got - ref).abs().max() / ref.abs().max()
+        assert err < 2e-6, (n_fft, float(err))

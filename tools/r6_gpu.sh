@@ -7,7 +7,9 @@
 #                      tests/test_gpu_resblock.py, per-launch sweep (r5 and each build), step A/B (in-tree vs builds)
 #   stamps LIB...      per-phase s_memtime stamps (libraries built with -DVQA_RS_STAMPS): backward d = 1, 9, 27 and
 #                      the forward, T = 32768
-#   close TAG          full GPU suite + smoke + round_profile.sh TAG on the in-tree library
+#   spec LIB...        spectral builds: tests, per-kernel averages, graph-timed target + loss/grad, step A/B
+#   suite              full GPU suite + smoke + the default bench line (in-tree library)
+#   close TAG          (VQA_COMMIT=<head>) full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
 NAME=$1; shift
 OUT=gpurun_out/r6_$NAME
@@ -55,7 +57,38 @@ stamps)
     VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/rs_stamps.py --T 32768 --d 1 9 27 2>&1 | grep -v amdgpu.ids || exit 1
     VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/rs_stamps.py --T 32768 --d 1 9 27 --fwd 2>&1 | grep -v amdgpu.ids || exit 1
   done ;;
+spec)
+  # spectral builds: tests/test_gpu_spectral.py on each, per-kernel averages (rocprofv3 --stats over tools/spec_one.py)
+  # and the graph-timed target + loss/grad for the r5 library and each build, then the step A/B
+  export TMPDIR=/tmp
+  for v in "$@"; do
+    VQA_LIB_PATH=$v timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+      tests/test_gpu_spectral.py > $OUT/t_$(basename $v).log 2>&1 || { tail -40 $OUT/t_$(basename $v).log; exit 1; }
+    echo "tests $v: $(tail -1 $OUT/t_$(basename $v).log)"
+  done
+  for v in variants/libvqa_r5.so "$@"; do
+    n=$(basename $v .so)
+    VQA_LIB_PATH=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$n -o t -- \
+      python tools/spec_one.py 5 > /dev/null 2> $OUT/$n.err || { tail -20 $OUT/$n.err; exit 1; }
+    echo "== $v: $(VQA_LIB_PATH=$v timeout -k 10 120 python tools/spec_one.py --time 2>/dev/null | head -1)"
+    python - "$OUT/$n/t_kernel_stats.csv" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "spec" in r["Name"]:
+        print(f"   {r['Name'][:60]:60s} calls {r['Calls']:>4s} avg {float(r['AverageNs'])/1e3:8.1f} us")
+PY
+    find $OUT/$n -name "*kernel_trace.csv" -delete
+  done
+  bash tools/ab_libs.sh 3 variants/libvqa_r5.so "$@" ;;
+suite)
+  timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \
+    || { tail -60 $OUT/suite.log; exit 1; }
+  tail -3 $OUT/suite.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -2 || exit 1
+  timeout -k 10 900 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/bench.json')); print(d['ms_per_step'], d['value'], d['roofline']['avg_launch_us'], {k: (v.get('ms_per_step'), v.get('value')) for k, v in d.items() if k.startswith('config')})" ;;
 close)
+  [ -n "$VQA_COMMIT" ] || { echo "close: set VQA_COMMIT (the git HEAD sent)"; exit 2; }
   TAG=$1
   timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \
     || { tail -60 $OUT/suite.log; exit 1; }

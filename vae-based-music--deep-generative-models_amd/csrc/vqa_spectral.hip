@@ -17,6 +17,7 @@
 // per (item, resolution) and a third overlap-adds the frame gradients (fixed summation order:
 // deterministic) and applies the scales. No atomics, no host sync, graph-capturable.
 #include "vqa_common.h"
+#include <utility>
 #include <algorithm>
 
 namespace vqa {
@@ -28,6 +29,9 @@ __device__ __forceinline__ f32x2 cmul(f32x2 a, f32x2 b) {
 }
 __device__ __forceinline__ f32x2 conj2(f32x2 a) { return f32x2{a.x, -a.y}; }
 __device__ __forceinline__ float cabs2(f32x2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+// |z| by the hardware square root (v_sqrt_f32, 1 ulp; the pair kernels): the correctly rounded sqrtf expands to a
+// scaling sequence (class test, selects, two multiplies) per value
+__device__ __forceinline__ float cabs_hw(f32x2 a) { return __builtin_amdgcn_sqrtf(a.x * a.x + a.y * a.y); }
 
 // Mixed-radix Stockham FFT in LDS: radix-8 stages while 8 divides the remaining length, then one radix-4 or
 // radix-2 stage (2048 = 8.8.8.4, 1024 = 8.8.8.2, 512 = 8.8.8: 4 / 4 / 3 passes through LDS instead of the
@@ -482,7 +486,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
         const f32x2 zk = z[pidx(k)], zm = z[pidx(km)];
         const f32x2 rka = f32x2{0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
         const f32x2 rkb = f32x2{0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x)};
-        const float mra = cabs2(rka), mrb = cabs2(rkb);
+        const float mra = cabs_hw(rka), mrb = cabs_hw(rkb);
         if constexpr (MAG) {
           if (acta) a.out[(size_t)fa * KB + k] = mra;
           if (actb) a.out[(size_t)fb * KB + k] = mrb;
@@ -562,6 +566,299 @@ __global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs
     // the next pair's pass 0 rewrites z: every read of it above precedes those stores in the wave's order
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Frame pairs by a FOUR-STEP FFT held in registers (round 6; N = 512, 1024, 2048): N = P x 64, P = N / 64 points per
+// lane, one wave per frame pair as above. Forward, with n = 64 n1 + n2, k = k1 + P k2:
+//   lane n2 loads z[64 n1 + n2] (n1 < P), P-point DFT over n1 in registers, times W_N^{n2 k1}
+//   -> ONE transpose through the wave's LDS buffer: the 64-point DFT of index k1 goes to the G = 64 / P lanes
+//      (k1, g), lane g holding n2 = g + G m (m < P)
+//   P-point DFT over m in registers, times W_64^{g q}, then a G-point DFT across the G lanes (radix-2 DPP stages:
+//      quad_perm / half-row mirror exchanges, no LDS) -> lane (k1, g) holds Z[k1 + P (q + P bitrev(g))], q < P
+//   the pair separation needs Z[N - k] beside Z[k]: ONE exchange through the LDS buffer (every lane writes its bins
+//      at their natural index, reads the mirror bins)
+// and the inverse (GRAD) runs the same steps backwards (cross-lane DIT, P-point DFT, W_N^{-n2 k1}, transpose,
+// P-point DFT, windowed stores of the frame gradients at n = lane + 64 n1). Three passes through LDS per pair where
+// the Stockham form makes five to seven, and its per-butterfly twiddle reads are replaced by one table row per
+// lane (W_N^{n2 k1} laid out [k1][n2] at a padded pitch) and compile-time constants. LDS layouts (8-byte slots):
+// the transpose rows have pitch 64 + G (the strided side hits 32 distinct slots per half wave) and the bin exchange
+// puts bin k at k + (k / P^2) 32 / G (both the own and the mirror accesses conflict-free, tools/spec4_banks.py).
+// Same loss / gradient definition and the same fp64-rounded twiddle and window tables as spec_pair_kernel.
+__device__ constexpr float kC32[32] = {
+    1.f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
+    0.55557023301960229f, 0.38268343236508984f, 0.19509032201612833f, 0.f, -0.19509032201612819f,
+    -0.38268343236508973f, -0.55557023301960196f, -0.70710678118654746f, -0.83146961230254535f,
+    -0.92387953251128674f, -0.98078528040323043f, -1.f, -0.98078528040323043f, -0.92387953251128685f,
+    -0.83146961230254546f, -0.70710678118654768f, -0.55557023301960218f, -0.38268343236509034f,
+    -0.19509032201612866f, 0.f, 0.1950903220161283f, 0.38268343236509f, 0.55557023301960184f,
+    0.70710678118654735f, 0.83146961230254524f, 0.92387953251128652f, 0.98078528040323032f};
+template <int E, bool INV> __device__ __forceinline__ f32x2 w32mul(f32x2 a) {
+  constexpr int e = E & 31;
+  if constexpr ((e & 1) == 0) {
+    return w16mul<e / 2, INV>(a);
+  } else {
+    const float c = kC32[e], sn = kC32[(e + 24) & 31];  // sin(2 pi e/32) = cos(2 pi (e - 8)/32)
+    return cmul(a, INV ? f32x2{c, sn} : f32x2{c, -sn});
+  }
+}
+template <bool INV, int... K>
+__device__ __forceinline__ void dft32_combine(f32x2 (&a)[32], const f32x2 (&ev)[16], const f32x2 (&od)[16],
+                                              std::integer_sequence<int, K...>) {
+  ((a[K] = ev[K] + w32mul<K, INV>(od[K]), a[K + 16] = ev[K] - w32mul<K, INV>(od[K])), ...);
+}
+// natural-order P-point DFT in registers (P = 32: two 16-point DFTs of the even / odd inputs and one combine)
+template <int P, bool INV> __device__ __forceinline__ void dftp(f32x2 (&a)[P]) {
+  if constexpr (P == 32) {
+    f32x2 ev[16], od[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ev[i] = a[2 * i];
+      od[i] = a[2 * i + 1];
+    }
+    dft<16, INV>(ev);
+    dft<16, INV>(od);
+    dft32_combine<INV>(a, ev, od, std::make_integer_sequence<int, 16>{});
+  } else {
+    dft<P, INV>(a);
+  }
+}
+// v of lane (lane ^ S) within groups of G <= 8 lanes (DPP: xor 1 / 2 by quad_perm, xor 4 by half-row mirror then
+// quad reverse)
+template <int S> __device__ __forceinline__ float xlane(float v) {
+  if constexpr (S == 1) return xl::xor1(v);
+  else if constexpr (S == 2) return xl::xor2(v);
+  else return xl::dpp<0x1B>(xl::hmirror(v));
+}
+template <int N> struct Spec4 {
+  static constexpr int P = N / 64, G = 64 / P, GB = G == 2 ? 1 : G == 4 ? 2 : 3, PITCH = 64 + G, BUF = N + 64;
+  static_assert(P * PITCH <= BUF && N + 32 <= BUF, "buffer plan");
+  // LDS slot of natural bin k in the exchange
+  static __device__ __forceinline__ int slot(int k) { return k + (k / (P * P)) * (32 / G); }
+};
+__device__ __forceinline__ int bitrev_n(int g, int bits) {
+  return bits == 1 ? g : bits == 2 ? (((g & 1) << 1) | (g >> 1)) : (((g & 1) << 2) | (g & 2) | (g >> 2));
+}
+// waves (frame pairs in flight) per workgroup, and whether the next pair's samples are prefetched into registers:
+// N = 2048 runs 8 waves (two per SIMD: a lone wave issues a VALU instruction every 4 cycles, two every 2) within
+// 256 VGPRs, which leaves no room for the 64-register prefetch; the smaller transforms prefetch and reach two or
+// more waves per SIMD through several 4-wave workgroups per CU
+template <int N> constexpr int spec4_waves() { return N == 2048 ? 8 : 4; }
+template <int N> constexpr bool spec4_prefetch() { return N != 2048; }
+
+// the G-point DFT across the lane group, forward (DIF: natural in, lane g holds output bitrev(g)) or inverse (DIT:
+// bitrev in, natural out); stage twiddles W_{2s}^{g mod s} from W_64 (tw64), upper lanes only (1 for the others)
+template <int N, bool INV>
+__device__ __forceinline__ void xlane_dft(f32x2 (&c)[N / 64], int g, const f32x2* tw64) {
+  typedef Spec4<N> S4;
+  constexpr int P = S4::P, G = S4::G;
+  auto stage = [&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    const bool up = (g & s) != 0;
+    const float sg = up ? -1.f : 1.f;
+    f32x2 w = f32x2{1.f, 0.f};
+    if constexpr (s > 1) {
+      if (up) w = tw64[(g & (s - 1)) * (32 / s)];
+      if (INV) w = conj2(w);
+    }
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      f32x2 u = c[q];
+      if constexpr (INV && s > 1) u = cmul(u, w);  // DIT: the upper input twiddled before the exchange
+      const f32x2 pv = f32x2{xlane<s>(u.x), xlane<s>(u.y)};
+      f32x2 r = f32x2{__builtin_fmaf(sg, u.x, pv.x), __builtin_fmaf(sg, u.y, pv.y)};  // lower u + p, upper p - u
+      if constexpr (!INV && s > 1) r = cmul(r, w);  // DIF: the upper output twiddled after it
+      c[q] = r;
+    }
+  };
+  if constexpr (!INV) {
+    if constexpr (G >= 8) stage(std::integral_constant<int, 4>{});
+    if constexpr (G >= 4) stage(std::integral_constant<int, 2>{});
+    stage(std::integral_constant<int, 1>{});
+  } else {
+    stage(std::integral_constant<int, 1>{});
+    if constexpr (G >= 4) stage(std::integral_constant<int, 2>{});
+    if constexpr (G >= 8) stage(std::integral_constant<int, 4>{});
+  }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int N, int MODE>
+__global__ __launch_bounds__(64 * spec4_waves<N>()) void spec_pair4_kernel(SpecPairArgs a) {
+  typedef Spec4<N> S4;
+  constexpr bool GRAD = MODE == PAIR_GRAD, MAG = MODE == PAIR_MAG, PREF = spec4_prefetch<N>();
+  constexpr int W = spec4_waves<N>();
+  constexpr int P = S4::P, G = S4::G, PITCH = S4::PITCH, KB = N / 2 + 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  f32x2* T = (f32x2*)smem;       // T[k1 PITCH + n2] = W_N^{n2 k1}
+  f32x2* tw64 = T + P * PITCH;   // W_64^e = W_N^{e P}
+  float* wn = (float*)(tw64 + 64);  // window, zero-padded to N
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  f32x2* buf = (f32x2*)(wn + N) + (size_t)wave * S4::BUF;
+  const f32x2* twg = (const f32x2*)a.tw;
+  for (int e = threadIdx.x; e < P * 64; e += 64 * W) {
+    const int k1 = e >> 6, n2 = e & 63;
+    T[k1 * PITCH + n2] = twg[n2 * k1];
+  }
+  for (int e = threadIdx.x; e < 64; e += 64 * W) tw64[e] = twg[e * P];
+  for (int e = threadIdx.x; e < N; e += 64 * W) wn[e] = e < a.win ? a.wn[e] : 0.f;
+  __syncthreads();
+
+  const int k1s = lane / G, g = lane & (G - 1), h = bitrev_n(g, S4::GB);
+  const int kbase = k1s + P * P * h;  // own bin of register q: kbase + P q
+  const int nframes = a.B * a.F, npairs = (nframes + 1) / 2;
+  const int gw = blockIdx.x * W + wave, nw = gridDim.x * W;
+  constexpr int NB = (KB + 63) / 64;
+  float ra[P], rb[P], ta[MAG ? 1 : NB], tb[MAG ? 1 : NB];
+  auto frame_base = [&](int f) {
+    const int bb_ = f / a.F;
+    return a.r + (size_t)bb_ * a.T + (size_t)(f - bb_ * a.F) * a.hop;
+  };
+  auto load_samples = [&](int pp) {
+    const float* sa = frame_base(min(2 * pp, nframes - 1));
+    const float* sb = frame_base(min(2 * pp + 1, nframes - 1));
+#pragma unroll
+    for (int n1 = 0; n1 < P; ++n1) {
+      const int n = lane + 64 * n1, nc = n < a.win ? n : 0;
+      ra[n1] = sa[nc];
+      rb[n1] = sb[nc];
+    }
+  };
+  if (PREF && gw < npairs) load_samples(gw);
+  for (int pp = gw; pp < npairs; pp += nw) {
+    const int fa = 2 * pp, fb = fa + 1;
+    const bool acta = fa < nframes, actb = fb < nframes;
+    if (!PREF) load_samples(pp);  // no prefetch: the other wave of the SIMD works meanwhile
+    if constexpr (!MAG) {
+      // target magnitudes of the lane's canonical bins lane + 64 j, requested now, used after the forward transform
+      const int pa = min(fa, nframes - 1), pb = min(fb, nframes - 1);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int k = lane + 64 * j, kc = k < KB ? k : 0;
+        ta[j] = a.tm[(size_t)pa * KB + kc];
+        tb[j] = a.tm[(size_t)pb * KB + kc];
+      }
+    }
+    f32x2 c[P];
+#pragma unroll
+    for (int n1 = 0; n1 < P; ++n1) {
+      const float w = wn[lane + 64 * n1];
+      c[n1] = f32x2{ra[n1] * w, rb[n1] * w};
+    }
+    // the next pair's samples: requested here for MAG (its bins are short), after the bins for LOSS / GRAD (their
+    // live range then spans only the inverse transform: fewer registers held through the forward one and the bins)
+    if (PREF && MAG && pp + nw < npairs) load_samples(pp + nw);
+    dftp<P, false>(c);  // over n1 -> k1
+#pragma unroll
+    for (int k1 = 1; k1 < P; ++k1) c[k1] = cmul(c[k1], T[k1 * PITCH + lane]);
+#pragma unroll
+    for (int k1 = 0; k1 < P; ++k1) buf[k1 * PITCH + lane] = c[k1];
+    wave_sync_lds();
+#pragma unroll
+    for (int m = 0; m < P; ++m) c[m] = buf[k1s * PITCH + g + G * m];
+    wave_sync_lds();
+    dftp<P, false>(c);  // over m -> q
+#pragma unroll
+    for (int q = 1; q < P; ++q) c[q] = cmul(c[q], tw64[g * q]);  // g = 0: W^0 = 1 exactly
+    xlane_dft<N, false>(c, g, tw64);  // lane (k1s, g): Z[kbase + P q]
+    // the bins: every lane writes its Z values at their natural slots, then takes canonical bins k = lane + 64 j
+    // (k <= N / 2: each once, as spec_pair_kernel) with their mirrors N - k; GRAD writes H at k and N - k back and
+    // every lane reads its own bins' H for the inverse
+#pragma unroll
+    for (int q = 0; q < P; ++q) buf[S4::slot(kbase + P * q)] = c[q];
+    wave_sync_lds();
+    float sda = 0.f, sxa = 0.f, sdb = 0.f, sxb = 0.f;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int k = lane + 64 * j;
+      if (NB * 64 == KB || k < KB) {
+        const int km = (N - k) & (N - 1);
+        const f32x2 zk = buf[S4::slot(k)], zm = buf[S4::slot(km)];
+        const f32x2 rka = f32x2{0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
+        const f32x2 rkb = f32x2{0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x)};
+        const float mra = cabs_hw(rka), mrb = cabs_hw(rkb);
+        if constexpr (MAG) {
+          if (acta) a.out[(size_t)fa * KB + k] = mra;
+          if (actb) a.out[(size_t)fb * KB + k] = mrb;
+        } else {
+          const float da = ta[j] - mra, db = tb[j] - mrb;
+          sda += da * da;
+          sxa += ta[j] * ta[j];
+          sdb += db * db;
+          sxb += tb[j] * tb[j];
+          if constexpr (GRAD) {
+            // dL/d(Re,Im)R_k = (|R|-|X|) R/|R| (0 at |R| = 0); H = H_a + i H_b, each the Hermitian extension of
+            // G/2 (G at k = 0, N/2) — spec_pair_kernel's values, written over Z at k and N - k at once: no later
+            // iteration reads those slots (its k and N - k lie in other 64-bin bands)
+            const float ga = mra > 0.f ? (mra - ta[j]) * __builtin_amdgcn_rcpf(mra) : 0.f;
+            const float gb = mrb > 0.f ? (mrb - tb[j]) * __builtin_amdgcn_rcpf(mrb) : 0.f;
+            const f32x2 Ga = f32x2{ga * rka.x, ga * rka.y}, Gb = f32x2{gb * rkb.x, gb * rkb.y};
+            if (k == 0 || k == N / 2) {
+              buf[S4::slot(k)] = f32x2{Ga.x, Gb.x};
+            } else {
+              buf[S4::slot(k)] = f32x2{0.5f * Ga.x - 0.5f * Gb.y, 0.5f * Ga.y + 0.5f * Gb.x};
+              buf[S4::slot(km)] = f32x2{0.5f * Ga.x + 0.5f * Gb.y, 0.5f * Gb.x - 0.5f * Ga.y};
+            }
+          }
+        }
+      }
+    }
+    if constexpr (GRAD) {
+      wave_sync_lds();
+#pragma unroll
+      for (int q = 0; q < P; ++q) c[q] = buf[S4::slot(kbase + P * q)];
+    }
+    wave_sync_lds();  // every read of buf precedes the next writes
+    if (PREF && !MAG && pp + nw < npairs) load_samples(pp + nw);
+    if constexpr (!MAG) {
+      sda = warp_sum(sda);
+      sxa = warp_sum(sxa);
+      sdb = warp_sum(sdb);
+      sxb = warp_sum(sxb);
+      if (lane == 0) {
+        if (acta) {
+          a.part[2 * (size_t)fa] = sda;
+          a.part[2 * (size_t)fa + 1] = sxa;
+        }
+        if (actb) {
+          a.part[2 * (size_t)fb] = sdb;
+          a.part[2 * (size_t)fb + 1] = sxb;
+        }
+      }
+    }
+    if constexpr (GRAD) {
+      xlane_dft<N, true>(c, g, tw64);  // lane (k1s, g): index g of the 64-point inverse, times W_64^{-g q}
+#pragma unroll
+      for (int q = 1; q < P; ++q) c[q] = cmul(c[q], conj2(tw64[g * q]));
+      dftp<P, true>(c);  // over q -> m: n2 = g + G m
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        const int e = k1s * PITCH + g + G * m;
+        c[m] = cmul(c[m], conj2(T[e]));
+        buf[e] = c[m];
+      }
+      wave_sync_lds();
+#pragma unroll
+      for (int k1 = 0; k1 < P; ++k1) c[k1] = buf[k1 * PITCH + lane];
+      wave_sync_lds();
+      dftp<P, true>(c);  // over k1 -> n1: h[lane + 64 n1]
+      float* oa = a.out + (size_t)fa * a.win;
+      float* ob = a.out + (size_t)fb * a.win;
+#pragma unroll
+      for (int n1 = 0; n1 < P; ++n1) {
+        const int n = lane + 64 * n1;
+        if (n < a.win) {
+          const float w = wn[n];
+          if (acta) oa[n] = c[n1].x * w;
+          if (actb) ob[n] = c[n1].y * w;
+        }
+      }
+    }
   }
 }
 
@@ -779,13 +1076,56 @@ static int launch_pairs(const SpecPairArgs& pa, hipStream_t s) {
   return VQA_OK;
 }
 
+// the four-step kernel: persistent, sized by the occupancy API as launch_pairs
+template <int N, int MODE>
+static int launch_pairs4(const SpecPairArgs& pa, hipStream_t s) {
+  typedef Spec4<N> S4;
+  const void* fn = (const void*)spec_pair4_kernel<N, MODE>;
+  constexpr int W = spec4_waves<N>();
+  const size_t lds = (size_t)(S4::P * S4::PITCH + 64) * sizeof(f32x2) + (size_t)N * sizeof(float) +
+                     (size_t)W * S4::BUF * sizeof(f32x2);
+  static size_t lds_set = 0;
+  if (lds > 65536 && lds > lds_set) {
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("spectral: cannot reserve %zu B of LDS", lds);
+      return VQA_E_UNSUPPORTED;
+    }
+    lds_set = lds;
+  }
+  const int npairs = (pa.B * pa.F + 1) / 2;
+  const int groups = (npairs + W - 1) / W;
+  static int cus = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
+  }();
+  static size_t occ_lds = 0;
+  static int per_cu = 1;
+  if (occ_lds != lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds) != hipSuccess || per_cu <= 0) {
+      (void)hipGetLastError();
+      per_cu = 1;
+    }
+    occ_lds = lds;
+  }
+  const int grid = std::min(groups, cus * per_cu);
+  hipLaunchKernelGGL((spec_pair4_kernel<N, MODE>), dim3(grid), dim3(64 * W), lds, s, pa);
+  VQA_LAUNCHED("spec_pair4_kernel");
+  return VQA_OK;
+}
+
 template <int MODE>
 static int dispatch_pairs(int n_fft, const SpecPairArgs& pa, hipStream_t s) {
   switch (n_fft) {
+    // the four-step form where it is faster (2048: 8 waves, two per SIMD, 84 -> 58 us per gradient launch at config 2);
+    // the Stockham form (one radix-8 / 16 / 4 pass per LDS round trip) keeps fewer VALU instructions per pair for
+    // the shorter transforms, which run at several waves per SIMD either way (round 6, profiles/r6_spectral.txt)
     case 256: return launch_pairs<256, MODE>(pa, s);
     case 512: return launch_pairs<512, MODE>(pa, s);
     case 1024: return launch_pairs<1024, MODE>(pa, s);
-    case 2048: return launch_pairs<2048, MODE>(pa, s);
+    case 2048: return launch_pairs4<2048, MODE>(pa, s);
     default: set_error("spectral: n_fft %d unsupported (256, 512, 1024, 2048)", n_fft); return VQA_E_UNSUPPORTED;
   }
 }
