@@ -441,7 +441,7 @@ def test_bench_py_bare_gpus2_spawns_ranks(cuda):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env.update(VQA_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-           "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior --no-fp32", "--no-roofline"]
+           "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior", "--no-fp32", "--no-roofline"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

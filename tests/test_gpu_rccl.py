@@ -113,7 +113,7 @@ def test_bench_py_rccl_branch_one_process(cuda, overlap):
         env.pop(k)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3",
-           "--warmup", "2", "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior --no-fp32", "--no-roofline"]
+           "--warmup", "2", "--batch", "2", "--seq", "8192", "--no-cpu-baseline", "--no-prior", "--no-fp32", "--no-roofline"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
     assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
     assert _rccl_lines(p.stdout + p.stderr), "no RCCL log line from bench.py's process group"
