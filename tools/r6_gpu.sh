@@ -8,6 +8,7 @@
 #   stamps LIB...      per-phase s_memtime stamps (libraries built with -DVQA_RS_STAMPS): backward d = 1, 9, 27 and
 #                      the forward, T = 32768
 #   spec LIB...        spectral builds: tests, per-kernel averages, graph-timed target + loss/grad, step A/B
+#   rsweep LIB...      per-launch residual-block sweep, r5 and each build
 #   suite              full GPU suite + smoke + the default bench line (in-tree library)
 #   close TAG          (VQA_COMMIT=<head>) full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
@@ -80,6 +81,13 @@ PY
     find $OUT/$n -name "*kernel_trace.csv" -delete
   done
   bash tools/ab_libs.sh 3 variants/libvqa_r5.so "$@" ;;
+rsweep)
+  # per-launch residual-block times only (tools/resblock_sweep.py --fused-only), the r5 library and each build
+  for v in variants/libvqa_r5.so "$@"; do
+    echo "== sweep $v"
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/resblock_sweep.py --T 32768 8192 2048 512 --reps 10 --fused-only 2>&1 \
+      | grep -v amdgpu.ids || exit 1
+  done ;;
 suite)
   timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \
     || { tail -60 $OUT/suite.log; exit 1; }

@@ -24,8 +24,9 @@ namespace vqa {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// complex product with fused multiply-adds (4 VALU instead of 6; one rounding less per component)
 __device__ __forceinline__ f32x2 cmul(f32x2 a, f32x2 b) {
-  return f32x2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+  return f32x2{__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x)};
 }
 __device__ __forceinline__ f32x2 conj2(f32x2 a) { return f32x2{a.x, -a.y}; }
 __device__ __forceinline__ float cabs2(f32x2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
@@ -389,10 +390,16 @@ __device__ __forceinline__ void wpass(f32x2* z, const f32x2* tw, int lane) {
     if (NBF % 64 == 0 || j < NBF) {
       const int p = j / S, q = j - p * S;
       dft<R, INV>(v[it]);
-      f32x2 w[R];
-      pass_twiddles<R, INV>(w, tw, p * S);
+      if constexpr (m == 1) {
+        // the last pass (p = 0): every twiddle is W^0
 #pragma unroll
-      for (int k = 0; k < R; ++k) z[pidx(q + S * (R * p + k))] = k ? cmul(v[it][k], w[k]) : v[it][k];
+        for (int k = 0; k < R; ++k) z[pidx(q + S * k)] = v[it][k];
+      } else {
+        f32x2 w[R];
+        pass_twiddles<R, INV>(w, tw, p * S);
+#pragma unroll
+        for (int k = 0; k < R; ++k) z[pidx(q + S * (R * p + k))] = k ? cmul(v[it][k], w[k]) : v[it][k];
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
