@@ -202,18 +202,43 @@ __device__ __forceinline__ uint4 mask_pos8(uint4 d, uint4 r) {
   return uint4{mask_pos_pk(d.x, r.x), mask_pos_pk(d.y, r.y), mask_pos_pk(d.z, r.z), mask_pos_pk(d.w, r.w)};
 }
 
-// weights -> LDS image [3][32][WS] of A operands: image row k*32 + rs_arow(oc) holds the weights of the
-// conv's output channel oc over its input channels (natural order). TRANSPOSE=true: a forward conv
-// (output = Keras o, input = c); false: the transposed conv (output = c, input = o).
-template <class T, bool TRANSPOSE>
-__device__ __forceinline__ void stage_wimg(T* img, const float* w) {
-  constexpr int WS = rs_stride<T>();
-  for (int e = threadIdx.x; e < 3 * RC * RC; e += 256) {
-    // e enumerates the Keras layout: w[k][r][c] with r = input channel, c = output channel
-    const int k = e / (RC * RC), rem = e - k * RC * RC, r = rem / RC, c = rem - r * RC;
-    const int oc = TRANSPOSE ? c : r, ic = TRANSPOSE ? r : c;
-    img[(k * RC + rs_arow(oc)) * WS + ic] = (T)w[e];
+// bf16 weight images in LDS, built once per workgroup from coalesced 16-byte loads of the fp32 Keras kernel
+// (3, 32, 32) (round 6): every lane of every wave then reads each A fragment as ONE 16-byte LDS read, where each wave
+// used to gather its fragments itself by strided scalar global loads (48 per 6 fragments, repeated by all four
+// waves) — the same bf16 values, so the same MFMA operands and bit-identical results.
+//   NAT = true:  img[(k*32 + r) * kImgP + c] = w[k][r][c]  (rows = Keras dim 1: the transposed conv's A rows)
+//   NAT = false: img[(k*32 + c) * kImgP + r] = w[k][r][c]  (rows = Keras dim 2, the output channel: a conv's A rows)
+constexpr int kImgP = RC + 8;          // bf16 per image row (80 bytes, the tiles' pitch)
+constexpr int kImgRows = 3 * RC;      // rows per image
+template <bool NAT>
+__device__ __forceinline__ void stage_img(bf16* img, const f32x4 (&v)[3 * RC * RC / 4 / 256]) {
+#pragma unroll
+  for (int i = 0; i < 3 * RC * RC / 4 / 256; ++i) {
+    const int e = 4 * (threadIdx.x + 256 * i), k = e / (RC * RC), r = (e / RC) % RC, c = e % RC;  // c .. c + 3
+    if constexpr (NAT) {
+      *(uint2*)(img + (k * RC + r) * kImgP + c) =
+          uint2{pk_bf16(v[i][0], v[i][1]), pk_bf16(v[i][2], v[i][3])};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) img[(k * RC + c + q) * kImgP + r] = (bf16)v[i][q];
+    }
   }
+}
+__device__ __forceinline__ void load_w4(f32x4 (&v)[3 * RC * RC / 4 / 256], const float* w) {
+#pragma unroll
+  for (int i = 0; i < 3 * RC * RC / 4 / 256; ++i) v[i] = ((const f32x4*)w)[threadIdx.x + 256 * i];
+}
+// the lane's A fragments from an image: row = the output channel of (mt, m) (the map of load_wfrags), K slice kc
+template <bool KPERM>
+__device__ __forceinline__ void frags_from_img(bf16x8 (&wf)[3][2][1], const bf16* img) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kc = rs_kcol<bf16, KPERM>(lane);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int o = 8 * rs_sig(m >> 2) + 4 * mt + (m & 3);
+      wf[k][mt][0] = *(const bf16x8*)(img + (k * RC + o) * kImgP + kc);
+    }
 }
 
 // The tile loads go through a per-item buffer descriptor: the hardware range check returns zeros for rows
@@ -427,8 +452,22 @@ void resblock_fwd_kernel(ResArgs a) {
             tend = tbeg + a.tpw + ((int)blockIdx.x < a.textra);
   if (tbeg >= tend) return;
   typename Mfma<T>::frag wfa[3][2][rs_ncc<T>()], wfb[3][2][rs_ncc<T>()];
-  load_wfrags<T, kRsFwdKperm>(wfa, a.wa);
-  load_wfrags<T, kRsFwdKperm>(wfb, a.wb);
+  if constexpr (sizeof(T) == 2 && DT > 0) {
+    // the two conv images in the H region (2 x 96 rows of the tile's HR = 192), read before the prologue's barrier;
+    // H is first written after it
+    bf16* img = (bf16*)(X + (HR + 2 * DT) * XS);
+    f32x4 va[3 * RC * RC / 4 / 256], vb[3 * RC * RC / 4 / 256];
+    load_w4(va, a.wa);
+    load_w4(vb, a.wb);
+    stage_img<false>(img, va);
+    stage_img<false>(img + kImgRows * kImgP, vb);
+    __syncthreads();
+    frags_from_img<kRsFwdKperm>(wfa, img);
+    frags_from_img<kRsFwdKperm>(wfb, img + kImgRows * kImgP);
+  } else {
+    load_wfrags<T, kRsFwdKperm>(wfa, a.wa);
+    load_wfrags<T, kRsFwdKperm>(wfb, a.wb);
+  }
   const int pn = rs_pi(lane & 15), oc = rs_ocol(lane);
   f32x4 bav[2], bbv[2];
 #pragma unroll
@@ -595,8 +634,23 @@ __global__ __launch_bounds__(256 * HALVES) void resblock_bwd_kernel(ResArgs a) {
   };
   // conv_a's forward fragments (recompute h) on every wave; team W: conv_a^T (dx), team H: conv_b^T (dh)
   typename M::frag wfa[3][2][rs_ncc<T>()], wt[3][2][rs_ncc<T>()];
-  load_wfrags<T, true>(wfa, a.wa);
-  load_wfrags_t<T>(wt, team == 0 ? a.wa : a.wb);
+  if constexpr (sizeof(T) == 2) {
+    // three images in the H and D regions (3 x 96 rows of their 2 HR >= 288): conv_a (every wave's wfa), conv_a and
+    // conv_b transposed (team W's / team H's wt); read before the prologue's barrier, H / D first written after it
+    bf16* img = (bf16*)H;
+    f32x4 va[3 * RC * RC / 4 / 256], vb[3 * RC * RC / 4 / 256];
+    load_w4(va, a.wa);
+    load_w4(vb, a.wb);
+    stage_img<false>(img, va);
+    stage_img<true>(img + kImgRows * kImgP, va);
+    stage_img<true>(img + 2 * kImgRows * kImgP, vb);
+    __syncthreads();
+    frags_from_img<true>(wfa, img);
+    frags_from_img<true>(wt, img + (team == 0 ? 1 : 2) * kImgRows * kImgP);
+  } else {
+    load_wfrags<T, true>(wfa, a.wa);
+    load_wfrags_t<T>(wt, team == 0 ? a.wa : a.wb);
+  }
   const int pn = rs_pi(lane & 15), oc = rs_ocol(lane);
   f32x4 bav[2];
 #pragma unroll
