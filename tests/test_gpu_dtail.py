@@ -40,7 +40,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("B,T,Cu,dt", [(2, 64, 64, torch.float32), (3, 37, 64, torch.float32), (1, 1, 64, torch.float32),
                                        (2, 300, 48, torch.float32), (2, 64, 64, torch.bfloat16),
-                                       (4, 1000, 64, torch.bfloat16)])
+                                       (4, 1000, 64, torch.bfloat16),
+                                       (2, 70001, 64, torch.bfloat16)])  # several grid-stride passes, ragged last
 def test_forward_backward(cuda, B, T, Cu, dt):
     g = torch.Generator().manual_seed(B * 1000 + T)
     h = torch.randn(B, T, 32, generator=g).to(dt)

@@ -9,6 +9,8 @@
 #                      the forward, T = 32768
 #   spec LIB...        spectral builds: tests, per-kernel averages, graph-timed target + loss/grad, step A/B
 #   rsweep LIB...      per-launch residual-block sweep, r5 and each build
+#   sweepab LIB...     per-launch sweep of each build, then the step A/B (in-tree library as the base)
+#   dtab LIB...        decoder-tail builds: tests, launch times + digests, per-kernel averages, step A/B
 #   suite              full GPU suite + smoke + the default bench line (in-tree library)
 #   close TAG          (VQA_COMMIT=<head>) full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
@@ -88,6 +90,37 @@ rsweep)
     VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/resblock_sweep.py --T 32768 8192 2048 512 --reps 10 --fused-only 2>&1 \
       | grep -v amdgpu.ids || exit 1
   done ;;
+sweepab)
+  # per-launch residual-block sweep for each build, then the step A/B against the in-tree library
+  for v in "$@"; do
+    echo "== sweep $v"
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/resblock_sweep.py --T 32768 8192 4096 2048 512 --reps 10 --fused-only \
+      2>&1 | grep -v amdgpu.ids || exit 1
+  done
+  bash tools/ab_libs.sh 3 "$@" ;;
+dtab)
+  # decoder-tail builds: tests/test_gpu_dtail.py, launch times + digest (tools/dtail_one.py), per-kernel averages,
+  # then the step A/B against the in-tree library
+  export TMPDIR=/tmp
+  for v in "$@"; do
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+      tests/test_gpu_dtail.py > $OUT/t_$(basename $v).log 2>&1 || { tail -40 $OUT/t_$(basename $v).log; exit 1; }
+    echo "tests $v: $(tail -1 $OUT/t_$(basename $v).log)"
+  done
+  for v in vae-based-music--deep-generative-models_amd/libvqa.so "$@"; do
+    n=$(basename $v .so)
+    echo "== $v"
+    VQA_LIB_PATH=$v timeout -k 10 120 python -u tools/dtail_one.py 2>&1 | grep -v amdgpu.ids || exit 1
+    VQA_LIB_PATH=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$n -o t -- \
+      python tools/dtail_one.py > /dev/null 2> $OUT/$n.err || { tail -20 $OUT/$n.err; exit 1; }
+    python - "$OUT/$n/t_kernel_stats.csv" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    print(f"   {r['Name'][:60]:60s} calls {r['Calls']:>4s} avg {float(r['AverageNs'])/1e3:8.1f} us")
+PY
+    find $OUT/$n -name "*kernel_trace.csv" -delete
+  done
+  bash tools/ab_libs.sh 3 "$@" ;;
 suite)
   timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \
     || { tail -60 $OUT/suite.log; exit 1; }
