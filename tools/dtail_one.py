@@ -47,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
         byt = a.B * a.T * 32 * 2 + a.B * 2 * a.T * 4 + (a.B * a.T * 32 * 2 if name == "bwd" else 0)
-        print(f"dtail_{name} B={a.B} T={a.T}: {us:7.2f} us per call ({byt / us / 1e3:.2f} TB/s algorithmic)")
+        print(f"dtail_{name} B={a.B} T={a.T}: {us:7.2f} us per call ({byt / us / 1e6:.2f} TB/s algorithmic)")
     torch.cuda.synchronize()
     dig = hashlib.sha256()
     for t in [y, dh] + grads:

@@ -14,7 +14,8 @@
 // two layers; only the association of the sums differs (u is not rounded to the activation dtype).
 //
 // Lanes: 4 lanes per row, each owning 8 consecutive channels (one 16-byte bf16 chunk), 16 rows per wave
-// instruction; the 3-tap window re-reads neighbour rows through the caches.
+// instruction. The forward loads every h row once (per-row tap dots, neighbours' terms exchanged across lanes); the
+// backward reads each row's dy window (6 values) per lane.
 #include "vqa_common.h"
 
 namespace vqa {
@@ -142,67 +143,138 @@ __device__ __forceinline__ int dt_part_row(int p, int P, int G) {
   return (p % R) * G + p / R;
 }
 
-// y[n, 2j + p] for 16 rows per wave and iteration; grid (row blocks, items), grid-stride over the item's rows
+// y[n, 2j + p], row-dot form: with A_a[p](i) = sum_c V[a][c][p] h[i][c] (three taps a = -1, 0, 1 -> index 0..2),
+//     y[2j + p] = bias + A_0[p](j - 1) + A_1[p](j) + A_2[p](j + 1)
+// so every h row is loaded ONCE. A lane quad owns kDtU consecutive rows (a wave 16 kDtU rows per pass); each lane
+// forms the six tap dots of its 8-channel slice per row, the neighbour rows' terms come from the same lane (inside the
+// quad's rows) or from the quads either side (ds_bpermute), and the wave's two halo rows (J0 - 1, J0 + 16 kDtU) are
+// loaded by the first / last quad; the 4 slices are then added in the quad (DPP) and lane q of the quad stores row q.
+// The next pass's loads are issued before this pass's arithmetic. Grid (row blocks, items), grid-stride over rows.
+constexpr int kDtU = 4;  // rows per lane quad and pass (= the quad's 4 lanes: one stored row each)
+__device__ __forceinline__ float dt_from_lane(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
 template <class T>
 __global__ __launch_bounds__(256) void dtail_fwd_kernel(DtArgs a) {
-  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3;
-  float v[3][8][2], e0[8], e1[8];
+  constexpr int U = kDtU;
+  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float v[3][8][2];
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int p = 0; p < 2; ++p) v[t][i][p] = a.comp[(t * DT_C + 8 * q + i) * 2 + p];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    e0[i] = a.comp[DT_NV + 8 * q + i];
-    e1[i] = a.comp[DT_NV + DT_C + 8 * q + i];
-  }
   const float bias = a.comp[DT_NV + 2 * DT_C], b0 = a.comp[DT_NV + 2 * DT_C + 1], b2 = a.comp[DT_NV + 2 * DT_C + 2];
   const T* H = (const T*)a.h + (size_t)blockIdx.y * a.T * DT_C;  // item n = blockIdx.y
   float* Y = a.y + (size_t)blockIdx.y * a.T * 2;
-  constexpr int U = 3;  // row groups of 16 per wave and iteration, all loads issued first (3: 136 VGPRs, 3 waves/SIMD)
   const int step = gridDim.x * 64 * U;
-  for (int J0 = blockIdx.x * 64 * U + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 16 * U; J0 < a.T;
-       J0 += step) {
-    Raw8<T> raw[U][3];
+  // loads from clamped addresses, zeros selected afterwards (no load in a branch: the wait before the arithmetic
+  // then counts only the previous pass's loads); the extra row is the halo (r = 0: J - 1, r = 15: J + 16U)
+  auto fetch = [&](int J, Raw8<T>(&raw)[U], Raw8<T>& rx) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = J0 + 16 * u + r;
-      const bool lv = j < a.T;
-      const T* hr = H + (size_t)j * DT_C + 8 * q;
-      raw[u][0].load(hr - DT_C, lv && j > 0);
-      raw[u][1].load(hr, lv);
-      raw[u][2].load(hr + DT_C, lv && j + 1 < a.T);
+      const int j = J + U * r + u;
+      const bool ok = j < a.T;
+      raw[u].load_sel(H + (size_t)(ok ? j : a.T - 1) * DT_C + 8 * q, ok);
     }
+    const int jx = r == 0 ? J - 1 : J + 16 * U;
+    const bool okx = (r == 0 || r == 15) && jx >= 0 && jx < a.T;
+    rx.load_sel(H + (size_t)(okx ? jx : 0) * DT_C + 8 * q, okx);
+  };
+  int J0 = blockIdx.x * 64 * U + wave * 16 * U;
+  Raw8<T> raw[U], rx;
+  fetch(J0, raw, rx);
+  for (; J0 < a.T; J0 += step) {
+    Raw8<T> rawn[U], rxn;
+    fetch(J0 + step, rawn, rxn);  // past the item: clamped addresses, zeros
+    float A[U][3][2];  // this lane's slice of the three tap dots of its U rows
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = J0 + 16 * u + r;
-      float hm[8], h0[8], hp[8];
-      raw[u][0].get(hm);
-      raw[u][1].get(h0);
-      raw[u][2].get(hp);
-      float y0 = 0.f, y1 = 0.f, c0 = 0.f, c1 = 0.f;
+      float h[8];
+      raw[u].get(h);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        y0 += v[0][i][0] * hm[i] + v[1][i][0] * h0[i] + v[2][i][0] * hp[i];
-        y1 += v[0][i][1] * hm[i] + v[1][i][1] * h0[i] + v[2][i][1] * hp[i];
-        c0 += e0[i] * h0[i];
-        c1 += e1[i] * h0[i];
-      }
-      if (j == 0) y0 -= c0;        // out conv padding at t = 0 drops tap k = 0
-      if (j == a.T - 1) y1 -= c1;  // ... and at t = 2T - 1 tap k = 2
-      // the quad's 4 channel slices (DPP quad permutes; see xl in vqa_common.h)
-      y0 += xl::xor1(y0);
-      y1 += xl::xor1(y1);
-      y0 += xl::xor2(y0);
-      y1 += xl::xor2(y1);
-      if (j < a.T && q == 0) {
-        y0 += bias - (j == 0 ? b0 : 0.f);
-        y1 += bias - (j == a.T - 1 ? b2 : 0.f);
-        *(float2*)(Y + (size_t)j * 2) = make_float2(y0, y1);
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          float s = v[t][0][p] * h[0];
+#pragma unroll
+          for (int i = 1; i < 8; ++i) s += v[t][i][p] * h[i];
+          A[u][t][p] = s;
+        }
+    }
+    // halo row: tap 0 of row J0 - 1 (first quad) or tap 2 of row J0 + 16U (last quad)
+    float X[2];
+    {
+      float h[8];
+      rx.get(h);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float s = (r == 0 ? v[0][0][p] : v[2][0][p]) * h[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) s += (r == 0 ? v[0][i][p] : v[2][i][p]) * h[i];
+        X[p] = s;
       }
     }
+    float pm[2], pp[2];  // the previous row's tap-0 and the next row's tap-2 slices for rows u = 0 and U - 1
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      pm[p] = dt_from_lane(A[U - 1][0][p], (lane - 4) & 63);
+      pp[p] = dt_from_lane(A[0][2][p], (lane + 4) & 63);
+      if (r == 0) pm[p] = X[p];
+      if (r == 15) pp[p] = X[p];
+    }
+    float y[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        y[u][p] = ((u == 0 ? pm[p] : A[u - 1][0][p]) + A[u][1][p]) + (u == U - 1 ? pp[p] : A[u + 1][2][p]);
+      const int j = J0 + U * r + u;
+      if (j == 0 || j == a.T - 1) {
+        // the out conv's padding at t = 0 drops tap k = 0, at t = 2T - 1 tap k = 2 (edge vectors of comp)
+        float h[8];
+        raw[u].get(h);
+        const int p = j == 0 ? 0 : 1;
+        const float* e = a.comp + DT_NV + p * DT_C + 8 * q;
+        float c = e[0] * h[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) c += e[i] * h[i];
+        if (j == 0) y[u][0] -= c;
+        if (j == a.T - 1) {
+          if (j == 0) {  // T = 1: both corrections on the same row
+            const float* e1 = a.comp + DT_NV + DT_C + 8 * q;
+            float c1 = e1[0] * h[0];
+#pragma unroll
+            for (int i = 1; i < 8; ++i) c1 += e1[i] * h[i];
+            y[u][1] -= c1;
+          } else {
+            y[u][1] -= c;
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        y[u][p] += xl::xor1(y[u][p]);
+        y[u][p] += xl::xor2(y[u][p]);
+      }
+    }
+    // lane q of the quad stores row U r + q: 64 consecutive rows' (y[2j], y[2j+1]) per wave store
+    float o0 = y[0][0], o1 = y[0][1];
+#pragma unroll
+    for (int u = 1; u < U; ++u) {
+      o0 = q == u ? y[u][0] : o0;
+      o1 = q == u ? y[u][1] : o1;
+    }
+    const int j = J0 + U * r + q;
+    if (j < a.T) {
+      o0 += bias - (j == 0 ? b0 : 0.f);
+      o1 += bias - (j == a.T - 1 ? b2 : 0.f);
+      *(float2*)(Y + (size_t)j * 2) = make_float2(o0, o1);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) raw[u] = rawn[u];
+    rx = rxn;
   }
 }
 
@@ -423,10 +495,16 @@ __global__ __launch_bounds__(256) void dtail_chain_kernel(const float* red, cons
 // U = 3 = 192, the backward's 4 x 16 x U = 2 = 128), about 1024 workgroups in all (4 resident per CU); one partial
 // row per workgroup in the backward
 constexpr int kDtGroups = 16;  // stage-1 groups of the backward's partial-row reduction
+// backward workgroups over all items: one round of 2 per CU (205 VGPRs: 2 waves per SIMD). 1024 (two rounds) took
+// 41.8 us per launch at B = 32, T = 32768, 512 38.3 us (768 forward / 512 backward A/B, profiles/r6_dtail.txt)
+constexpr int kDtBwdWgs = 512;
+// forward workgroups over all items: one round of 3 per CU (154 VGPRs); 1024 took 19.8 us, 768 18.7 us (the
+// neighbour-load form before: 24.8 us)
+constexpr int kDtFwdWgs = 768;
 
-static int dt_gx(int B, int T, int rows_per_block) {
+static int dt_gx(int B, int T, int rows_per_block, int total) {
   const int per_item = (T + rows_per_block - 1) / rows_per_block;
-  int gx = 1024 / B;
+  int gx = total / B;
   if (gx > per_item) gx = per_item;
   return gx > 0 ? gx : 1;
 }
@@ -445,7 +523,7 @@ extern "C" size_t vqa_dtail_workspace(int B, int T, int C, int Cu, int dtype) {
   (void)C;
   (void)Cu;
   (void)dtype;
-  const size_t g = (size_t)dt_gx(B, T, 128) * B;  // the backward's partial rows (+ the stage-1 group sums)
+  const size_t g = (size_t)dt_gx(B, T, 128, kDtBwdWgs) * B;  // the backward's partial rows (+ the stage-1 group sums)
   return ((size_t)DT_COMP + (size_t)DT_PART + (g + kDtGroups) * DT_PART) * sizeof(float);
 }
 
@@ -463,7 +541,7 @@ extern "C" int vqa_dtail_fwd(const void* h, const float* w_up, const float* b_up
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
   DtArgs a{h, nullptr, y, nullptr, comp, nullptr, B, T, 0};
-  const dim3 g(dt_gx(B, T, 192), B);
+  const dim3 g(dt_gx(B, T, 64 * kDtU, kDtFwdWgs), B);
   if (dtype == VQA_BF16) hipLaunchKernelGGL(dtail_fwd_kernel<bf16>, g, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dtail_fwd_kernel<float>, g, dim3(256), 0, s, a);
   VQA_LAUNCHED("dtail_fwd_kernel");
@@ -486,7 +564,7 @@ extern "C" int vqa_dtail_bwd(const float* dy, const void* h, const float* w_up, 
   hipLaunchKernelGGL(dtail_compose_kernel, dim3((DT_COMP_WAVES + 3) / 4), dim3(256), 0, s, w_up, b_up, w_out, b_out,
                      Cu, comp);
   VQA_LAUNCHED("dtail_compose_kernel");
-  const dim3 g(dt_gx(B, T, 128), B);
+  const dim3 g(dt_gx(B, T, 128, kDtBwdWgs), B);
   // many partial rows of few columns: reduced in two fixed-order stages (a single 1024-deep pass over 2 column
   // blocks was a 23 us serial chain of row loads at the head of every level's backward)
   const int P = (int)(g.x * g.y), G = (P >= 4 * kDtGroups && P % kDtGroups == 0) ? kDtGroups : 0;
