@@ -42,11 +42,12 @@ def main():
     B, T, O, K, S = a.batch, a.T, 32, 4, 2
     To = T // S
     pad = max((To - 1) * S + K - T, 0) // 2
-    x = torch.randn(B, T, 1, device=dev)
-    w = torch.randn(K, 1, O, device=dev) * 0.3
-    b = torch.zeros(O, device=dev)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(B, T, 1, device=dev, generator=g)
+    w = torch.randn(K, 1, O, device=dev, generator=g) * 0.3
+    b = torch.randn(O, device=dev, generator=g) * 0.1
     y = torch.empty(B, To, O, device=dev, dtype=torch.bfloat16)
-    dy = torch.randn(B, To, O, device=dev).to(torch.bfloat16)
+    dy = torch.randn(B, To, O, device=dev, generator=g).to(torch.bfloat16)
     dw, db = torch.empty(K, 1, O, device=dev), torch.empty(O, device=dev)
     fl = V.X_F32
     f_us = timed(lambda: V.conv1d_fwd(x, w, b, None, y, B, T, To, 1, O, K, S, 1, pad, fl, V.BF16), a.reps)
@@ -60,6 +61,12 @@ def main():
     mb_w = (x.numel() * 4 + dy.numel() * 2) / 1e6
     print(f"first conv B={B} T={T}: fwd {f_us:.1f} us ({mb_f / f_us:.2f} TB/s of {mb_f:.0f} MB)  "
           f"wgrad+reduce {w_us:.1f} us ({mb_w / w_us:.2f} TB/s of {mb_w:.0f} MB)", flush=True)
+    import hashlib
+    dig = hashlib.sha256()
+    for t in (y, dw, db):
+        c = t.detach().cpu().contiguous()
+        dig.update((c.view(torch.int16) if c.dtype == torch.bfloat16 else c.view(torch.int32)).numpy().tobytes())
+    print(f"digest {dig.hexdigest()[:16]} (y, dW, db; {V.LIB_PATH})")
 
 
 if __name__ == "__main__":

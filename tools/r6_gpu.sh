@@ -11,6 +11,7 @@
 #   rsweep LIB...      per-launch residual-block sweep, r5 and each build
 #   sweepab LIB...     per-launch sweep of each build, then the step A/B (in-tree library as the base)
 #   dtab LIB...        decoder-tail builds: tests, launch times + digests, per-kernel averages, step A/B
+#   convab LIB...      waveform-end conv builds: conv tests, first-conv times + digests, per-kernel averages, step A/B
 #   suite              full GPU suite + smoke + the default bench line (in-tree library)
 #   close TAG          (VQA_COMMIT=<head>) full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
@@ -117,6 +118,30 @@ dtab)
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
     print(f"   {r['Name'][:60]:60s} calls {r['Calls']:>4s} avg {float(r['AverageNs'])/1e3:8.1f} us")
+PY
+    find $OUT/$n -name "*kernel_trace.csv" -delete
+  done
+  bash tools/ab_libs.sh 3 "$@" ;;
+convab)
+  # waveform-end conv builds: tests/test_gpu_conv.py on each, the first conv's forward / weight-gradient times and
+  # output digest (tools/first_conv.py) for the in-tree library and each build, per-kernel averages, step A/B
+  export TMPDIR=/tmp
+  for v in "$@"; do
+    VQA_LIB_PATH=$v timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+      tests/test_gpu_conv.py > $OUT/t_$(basename $v).log 2>&1 || { tail -40 $OUT/t_$(basename $v).log; exit 1; }
+    echo "tests $v: $(tail -1 $OUT/t_$(basename $v).log)"
+  done
+  for v in vae-based-music--deep-generative-models_amd/libvqa.so "$@"; do
+    n=$(basename $v .so)
+    echo "== $v"
+    VQA_LIB_PATH=$v timeout -k 10 120 python -u tools/first_conv.py 2>&1 | grep -v amdgpu.ids || exit 1
+    VQA_LIB_PATH=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$n -o t -- \
+      python tools/first_conv.py > /dev/null 2> $OUT/$n.err || { tail -20 $OUT/$n.err; exit 1; }
+    python - "$OUT/$n/t_kernel_stats.csv" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "vqa" in r["Name"]:
+        print(f"   {r['Name'][:60]:60s} calls {r['Calls']:>4s} avg {float(r['AverageNs'])/1e3:8.1f} us")
 PY
     find $OUT/$n -name "*kernel_trace.csv" -delete
   done

@@ -1034,6 +1034,33 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* v)
   *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
 
+// buffer loads converting to fp32 (an out-of-range offset reads zeros)
+template <class T> __device__ __forceinline__ float ld1_buf(__amdgpu_buffer_rsrc_t r, int off);
+template <> __device__ __forceinline__ float ld1_buf<float>(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ float ld1_buf<bf16>(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0) << 16);
+}
+template <class T> __device__ __forceinline__ void ld8_buf(__amdgpu_buffer_rsrc_t r, int off, float* v);
+template <> __device__ __forceinline__ void ld8_buf<bf16>(__amdgpu_buffer_rsrc_t r, int off, float* v) {
+  const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+template <> __device__ __forceinline__ void ld8_buf<float>(__amdgpu_buffer_rsrc_t r, int off, float* v) {
+  const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = __uint_as_float(a[i]);
+    v[i + 4] = __uint_as_float(b[i]);
+  }
+}
+
 // NM: the narrow side's width bound (1 for the model's 1-channel ends: half the accumulators and tap registers of
 // NM = 2, 29.4 vs 33.6 us for the first encoder conv at cfg2, the same sums in the same order)
 template <class TX, class TG, bool WIDE_X, int NM>
@@ -1046,8 +1073,10 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
   const int n = blockIdx.y, ch = blockIdx.x;
   const int tbeg = ch * a.CH, tend = min(a.T_out, tbeg + a.CH);
   const bool relu = a.flags & VQA_PRE_RELU;
-  const TX* X = (const TX*)a.x + (long long)n * a.T_in * a.C;
-  const TG* G = (const TG*)a.g + (long long)n * a.T_out * a.O;
+  // the item's rows as buffer resources (host-checked: an item is < 2^30 bytes)
+  const unsigned xbytes = (unsigned)a.T_in * a.C * (unsigned)sizeof(TX), gbytes = (unsigned)a.T_out * a.O * (unsigned)sizeof(TG);
+  const __amdgpu_buffer_rsrc_t rx = item_rsrc(a.x, (long long)n * xbytes, xbytes);
+  const __amdgpu_buffer_rsrc_t rg = item_rsrc(a.g, (long long)n * gbytes, gbytes);
   float acc[KM][NM][8];
   float bacc[8];
 #pragma unroll
@@ -1065,29 +1094,28 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WgradArgs a) {
       float xv[U][KM][WIDE_X ? 8 : NM];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        // every load issued unconditionally: rows past the chunk and taps outside the item get an out-of-range
+        // buffer offset (kOOB), which reads zeros (a load in a branch was waited for right there: 8 serial round
+        // trips per iteration, 33 us at the first conv)
         const int tt = t + u * RL;
         const bool okr = tt < tend;
+        const int goff = okr ? (tt * a.O + (WIDE_X ? 0 : v * 8)) * (int)sizeof(TG) : kOOB;
         if (WIDE_X) {
 #pragma unroll
-          for (int i = 0; i < NM; ++i) gv[u][i] = (okr && i < NN) ? ld(G + (long long)tt * a.O + i) : 0.f;
+          for (int i = 0; i < NM; ++i) gv[u][i] = ld1_buf<TG>(rg, i < NN ? goff + i * (int)sizeof(TG) : kOOB);
         } else {
-          if (okr) ld8(G + (long long)tt * a.O + v * 8, gv[u]);
-          else
-#pragma unroll
-            for (int j = 0; j < 8; ++j) gv[u][j] = 0.f;
+          ld8_buf<TG>(rg, goff, gv[u]);
         }
 #pragma unroll
         for (int k = 0; k < KM; ++k) {
           const int ti = tt * a.S + k * a.D - a.P;
           const bool ok = okr && k < a.K && ti >= 0 && ti < a.T_in;
+          const int xoff = ok ? (ti * a.C + (WIDE_X ? v * 8 : 0)) * (int)sizeof(TX) : kOOB;
           if (WIDE_X) {
-            if (ok) ld8(X + (long long)ti * a.C + v * 8, xv[u][k]);
-            else
-#pragma unroll
-              for (int j = 0; j < 8; ++j) xv[u][k][j] = 0.f;
+            ld8_buf<TX>(rx, xoff, xv[u][k]);
           } else {
 #pragma unroll
-            for (int i = 0; i < NM; ++i) xv[u][k][i] = (ok && i < NN) ? ld(X + (long long)ti * a.C + i) : 0.f;
+            for (int i = 0; i < NM; ++i) xv[u][k][i] = ld1_buf<TX>(rx, i < NN ? xoff + i * (int)sizeof(TX) : kOOB);
           }
         }
       }
@@ -1602,27 +1630,49 @@ static int launch_gather_thin(const GatherArgs& a, hipStream_t s) {
 // (bf16) store — consecutive lanes write consecutive bytes. Per-row tap order k = 0..K-1 (as the gather
 // kernels).
 constexpr int CI1_RB = 512, CI1_KMAX = 8;
+// input values staged per thread by the unrolled path (span <= 256 CI1_SPT: stride 2, K <= 4 at CI1_RB = 512); the
+// loads are issued together from clamped addresses, zeros selected (the loop form waited on every load in turn)
+constexpr int CI1_SPT = 5;
 
-template <class TX, class TY, int O>
+// KT: the tap count as a compile-time constant (4: the model's first conv; fewer registers, all tap reads issued
+// together) or 0 (any K <= CI1_KMAX from the arguments). Same sums in the same order either way.
+template <class TX, class TY, int O, int KT>
 __global__ __launch_bounds__(256) void gather_ci1_kernel(GatherArgs a) {
   constexpr int L = O / 8, RPP = 256 / L;  // lanes per row, rows per pass
+  constexpr int KK = KT > 0 ? KT : CI1_KMAX;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* xl = (float*)smem;
   const int n = blockIdx.y, t0 = blockIdx.x * CI1_RB;
   const int span = (CI1_RB - 1) * a.S + (a.K - 1) * a.D + 1, i0 = t0 * a.S - a.P;
   const TX* X = (const TX*)a.x + (size_t)n * a.T_in;
   const bool relu = a.flags & VQA_PRE_RELU;
-  for (int e = threadIdx.x; e < span; e += 256) {
-    const int ti = i0 + e;
-    float v = (ti >= 0 && ti < a.T_in) ? ld(X + ti) : 0.f;
-    xl[e] = relu ? fmaxf(v, 0.f) : v;
+  if (span <= 256 * CI1_SPT) {
+    float v[CI1_SPT];
+#pragma unroll
+    for (int i = 0; i < CI1_SPT; ++i) {
+      const int e = threadIdx.x + 256 * i, ti = i0 + e;
+      const bool ok = e < span && ti >= 0 && ti < a.T_in;
+      const float x = ld(X + min(max(ti, 0), a.T_in - 1));
+      v[i] = ok ? x : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CI1_SPT; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e < span) xl[e] = relu ? fmaxf(v[i], 0.f) : v[i];
+    }
+  } else {
+    for (int e = threadIdx.x; e < span; e += 256) {
+      const int ti = i0 + e;
+      float v = (ti >= 0 && ti < a.T_in) ? ld(X + ti) : 0.f;
+      xl[e] = relu ? fmaxf(v, 0.f) : v;
+    }
   }
   const int o8 = (threadIdx.x % L) * 8, rl = threadIdx.x / L;
-  float w[CI1_KMAX][8], b[8];
+  float w[KK][8], b[8];
 #pragma unroll
-  for (int k = 0; k < CI1_KMAX; ++k)
+  for (int k = 0; k < KK; ++k)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[k][j] = k < a.K ? a.w[k * O + o8 + j] : 0.f;
+    for (int j = 0; j < 8; ++j) w[k][j] = (KT > 0 || k < a.K) ? a.w[k * O + o8 + j] : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) b[j] = a.bias ? a.bias[o8 + j] : 0.f;
   __syncthreads();
@@ -1632,8 +1682,8 @@ __global__ __launch_bounds__(256) void gather_ci1_kernel(GatherArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
 #pragma unroll
-    for (int k = 0; k < CI1_KMAX; ++k) {
-      if (k >= a.K) break;
+    for (int k = 0; k < KK; ++k) {
+      if (KT == 0 && k >= a.K) break;
       const float xv = xl[r * a.S + k * a.D];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += xv * w[k][j];
@@ -1644,12 +1694,18 @@ __global__ __launch_bounds__(256) void gather_ci1_kernel(GatherArgs a) {
   }
 }
 
+template <class TX, class TY, int KT>
+static void launch_gather_ci1_k(const GatherArgs& a, const dim3& grid, size_t lds, hipStream_t s) {
+  if (a.O == 32) hipLaunchKernelGGL((gather_ci1_kernel<TX, TY, 32, KT>), grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL((gather_ci1_kernel<TX, TY, 64, KT>), grid, dim3(256), lds, s, a);
+}
+
 template <class TX, class TY>
 static int launch_gather_ci1(const GatherArgs& a, hipStream_t s) {
   const size_t lds = (size_t)((CI1_RB - 1) * a.S + (a.K - 1) * a.D + 1) * sizeof(float);
   const dim3 grid((a.T_out + CI1_RB - 1) / CI1_RB, a.B);
-  if (a.O == 32) hipLaunchKernelGGL((gather_ci1_kernel<TX, TY, 32>), grid, dim3(256), lds, s, a);
-  else hipLaunchKernelGGL((gather_ci1_kernel<TX, TY, 64>), grid, dim3(256), lds, s, a);
+  if (a.K == 4) launch_gather_ci1_k<TX, TY, 4>(a, grid, lds, s);
+  else launch_gather_ci1_k<TX, TY, 0>(a, grid, lds, s);
   VQA_LAUNCHED("gather_ci1_kernel");
   return VQA_OK;
 }
@@ -1712,6 +1768,8 @@ static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O,
   const bool anyf32 = (flags & (VQA_X_F32 | VQA_Y_F32)) != 0;
   const size_t esz = dtype == VQA_BF16 ? 2 : 4;
   p.nb = (flags & WG_DB_FROM_X) ? C : O;
+  // the thin kernels address an item's rows through 32-bit buffer offsets
+  const bool thin_fits = (long long)T_in * C * 4 < (1ll << 30) && (long long)T_out * O * 4 < (1ll << 30);
   if (!anyf32 && (C == 32 || C == 64) && (O == 32 || O == 64) && K <= 4) {
     p.kind = WG_MFMA;
     p.TT = dtype == VQA_BF16 ? 128 : 64;
@@ -1722,11 +1780,11 @@ static WgradPlan plan_wgrad(int dtype, int B, int T_in, int T_out, int C, int O,
       const int r2 = (p.TT - 1) * S + (K - 1) * D + 1;
       p.lds = ((size_t)p.TT * (O + 16 / esz) + (size_t)r2 * (C + 16 / esz)) * esz;
     }
-  } else if (K <= 4 && C % 8 == 0 && C <= 256 && O <= 2 && !(flags & WG_DB_FROM_X)) {
+  } else if (K <= 4 && C % 8 == 0 && C <= 256 && O <= 2 && !(flags & WG_DB_FROM_X) && thin_fits) {
     p.kind = WG_THIN_X;
     p.TT = 64;
     p.lds = (size_t)256 * (4 * 2 * 8 + 8) * sizeof(float);
-  } else if (K <= 4 && O % 8 == 0 && O <= 256 && C <= 2 && !(flags & WG_DB_FROM_X)) {
+  } else if (K <= 4 && O % 8 == 0 && O <= 256 && C <= 2 && !(flags & WG_DB_FROM_X) && thin_fits) {
     p.kind = WG_THIN_G;
     p.TT = 64;
     p.lds = (size_t)256 * (4 * 2 * 8 + 8) * sizeof(float);
