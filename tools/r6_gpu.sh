@@ -12,6 +12,7 @@
 #   sweepab LIB...     per-launch sweep of each build, then the step A/B (in-tree library as the base)
 #   dtab LIB...        decoder-tail builds: tests, launch times + digests, per-kernel averages, step A/B
 #   convab LIB...      waveform-end conv builds: conv tests, first-conv times + digests, per-kernel averages, step A/B
+#   sweeps LIB...      per-shape conv sweep of the in-tree library and each build, then the step A/B (ROUNDS)
 #   suite              full GPU suite + smoke + the default bench line (in-tree library)
 #   close TAG          (VQA_COMMIT=<head>) full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
@@ -146,6 +147,14 @@ PY
     find $OUT/$n -name "*kernel_trace.csv" -delete
   done
   bash tools/ab_libs.sh 3 "$@" ;;
+sweeps)
+  # per-shape conv times of one eager step (tools/conv_sweep.py) for the in-tree library and each build, then the
+  # step A/B (ROUNDS rounds; env, default 3)
+  for v in vae-based-music--deep-generative-models_amd/libvqa.so "$@"; do
+    echo "== conv sweep $v"
+    VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/conv_sweep.py 2>&1 | grep -v amdgpu.ids || exit 1
+  done
+  bash tools/ab_libs.sh ${ROUNDS:-3} "$@" ;;
 suite)
   timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \
     || { tail -60 $OUT/suite.log; exit 1; }

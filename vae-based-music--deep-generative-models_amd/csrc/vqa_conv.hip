@@ -531,6 +531,10 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
     return src;
   };
 
+  // the bias per output channel (PAIR: both halves), staged once: the epilogue reads it from LDS (a global load
+  // per output block in the epilogue was waited for in turn: 8 serial round trips per tile at O = 128)
+  __shared__ __attribute__((aligned(16))) float bias_l[O];
+  for (int i = threadIdx.x; i < O; i += 256) bias_l[i] = a.bias ? a.bias[bias_index(a, i)] : 0.f;
   stage_weights<T, C, O>(a, wl, WS);
   TileSrc S0, S1;
   TileRegs<T, C, PV> A, B;
@@ -590,7 +594,7 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
         }
         f32x4 v = acc[mt][nt];
         if (a.bias) {
-          const float* bp = a.bias + bias_index(a, o);
+          const f32x4 bp = *(const f32x4*)(bias_l + o);
           v = f32x4{v[0] + bp[0], v[1] + bp[1], v[2] + bp[2], v[3] + bp[3]};
         }
         if (do_mask) {
@@ -927,7 +931,10 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
   const T* Gi = (const T*)a.g + (long long)n * a.T_out * O;
   const T* Xi = (const T*)a.x + (long long)n * a.T_in * C;
   RowStager<T, O, 4> sg;
-  RowStager<T, C, 4> sx;
+  // input chunks per thread: the model's input spans without the tail loop (whose loads were waited for one by one
+  // before every sub-tile's store): bf16 C = 32 stride 2 K = 4 (258 rows x 4 chunks) -> 5; C = 64 stride 1 K = 3
+  // (130 x 8) and stride 2 K = 4 (258 x 8) -> 9
+  RowStager<T, C, sizeof(T) == 2 ? (C == 32 ? 5 : (C == 64 ? 9 : 4)) : 4> sx;
   if (tbeg < tend) {
     const int nrows = min(TT, tend - tbeg);
     sg.load(Gi, tbeg, tbeg + nrows, tbeg, TT);
