@@ -71,7 +71,7 @@ spec)
       tests/test_gpu_spectral.py > $OUT/t_$(basename $v).log 2>&1 || { tail -40 $OUT/t_$(basename $v).log; exit 1; }
     echo "tests $v: $(tail -1 $OUT/t_$(basename $v).log)"
   done
-  for v in variants/libvqa_r5.so "$@"; do
+  for v in ${SPEC_BASE:-variants/libvqa_r5.so} "$@"; do
     n=$(basename $v .so)
     VQA_LIB_PATH=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$n -o t -- \
       python tools/spec_one.py 5 > /dev/null 2> $OUT/$n.err || { tail -20 $OUT/$n.err; exit 1; }
@@ -84,7 +84,7 @@ for r in csv.DictReader(open(sys.argv[1])):
 PY
     find $OUT/$n -name "*kernel_trace.csv" -delete
   done
-  bash tools/ab_libs.sh 3 variants/libvqa_r5.so "$@" ;;
+  bash tools/ab_libs.sh 3 ${SPEC_BASE:-variants/libvqa_r5.so} "$@" ;;
 rsweep)
   # per-launch residual-block times only (tools/resblock_sweep.py --fused-only), the r5 library and each build
   for v in variants/libvqa_r5.so "$@"; do

@@ -92,10 +92,28 @@ __global__ __launch_bounds__(256) void dtail_compose_kernel(const float* w_up, c
     float s = 0.f;
     if (e < DT_NV) {
       const int a = e / (2 * DT_C) - 1, c = (e >> 1) % DT_C, p = e & 1;
-      for (int k = 0; k < 3; ++k) {
-        const int kb = p + k - 2 * a;
-        if (kb < 0 || kb > 3) continue;
-        for (int o = lane; o < Cu; o += 64) s += w_out[k * Cu + o] * w_up[((size_t)kb * Cu + o) * DT_C + c];
+      if (Cu <= 64) {
+        // one channel per lane: the six loads issued together (clamped indices, unused terms skipped), the
+        // same products added in the same order as the loop below
+        const int o = min(lane, Cu - 1);
+        float wo[3], wu[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int kb = min(max(p + k - 2 * a, 0), 3);
+          wo[k] = w_out[k * Cu + o];
+          wu[k] = w_up[((size_t)kb * Cu + o) * DT_C + c];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int kb = p + k - 2 * a;
+          if (kb >= 0 && kb <= 3 && lane < Cu) s += wo[k] * wu[k];
+        }
+      } else {
+        for (int k = 0; k < 3; ++k) {
+          const int kb = p + k - 2 * a;
+          if (kb < 0 || kb > 3) continue;
+          for (int o = lane; o < Cu; o += 64) s += w_out[k * Cu + o] * w_up[((size_t)kb * Cu + o) * DT_C + c];
+        }
       }
     } else {
       const int c = (e - DT_NV) % DT_C, edge = (e - DT_NV) / DT_C;  // edge 0: (k=0, kb=0); 1: (k=2, kb=3)

@@ -406,8 +406,16 @@ __device__ __forceinline__ void wpass(f32x2* z, const f32x2* tw, int lane) {
   __builtin_amdgcn_wave_barrier();
 }
 
+// the target-magnitude launches (PAIR_MAG, no gradient half) at 5 / 3 waves per SIMD for N = 512 / 1024: their few
+// spilled registers cost less than the third round of pairs they save (512: 25.1 -> 21.6 us, 1024: 29.3 -> 26.5 us;
+// the gradient launches spill inside their passes at that occupancy and took twice as long, so they keep theirs;
+// profiles/r6_spectral_occ.txt)
+template <int N, int MODE> constexpr int spec_pair_min_waves() {
+  return MODE == PAIR_MAG ? (N == 512 ? 5 : (N == 1024 ? 3 : 1)) : 1;
+}
 template <int N, int MODE>
-__global__ __launch_bounds__(64 * kSpecWaves) void spec_pair_kernel(SpecPairArgs a) {
+__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_waves_per_eu(spec_pair_min_waves<N, MODE>(), 8)))
+void spec_pair_kernel(SpecPairArgs a) {
   constexpr bool GRAD = MODE == PAIR_GRAD, MAG = MODE == PAIR_MAG;
   constexpr int KB = N / 2 + 1, NB = (KB + 63) / 64;
   constexpr int R0 = wradix<N, 0>(), R1 = wradix<N, 1>(), R2 = wradix<N, 2>();
