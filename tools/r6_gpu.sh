@@ -13,6 +13,7 @@
 #   dtab LIB...        decoder-tail builds: tests, launch times + digests, per-kernel averages, step A/B
 #   convab LIB...      waveform-end conv builds: conv tests, first-conv times + digests, per-kernel averages, step A/B
 #   sweeps LIB...      per-shape conv sweep of the in-tree library and each build, then the step A/B (ROUNDS)
+#   priorab LIB...     prior builds: prior tests, then the config-4 train step alternating with the in-tree library
 #   suite              full GPU suite + smoke + the default bench line (in-tree library)
 #   close TAG          (VQA_COMMIT=<head>) full GPU suite + smoke + round_profile.sh TAG on the in-tree library
 set -o pipefail
@@ -155,6 +156,19 @@ sweeps)
     VQA_LIB_PATH=$v timeout -k 10 300 python -u tools/conv_sweep.py 2>&1 | grep -v amdgpu.ids || exit 1
   done
   bash tools/ab_libs.sh ${ROUNDS:-3} "$@" ;;
+priorab)
+  # prior builds: tests/test_gpu_prior.py on each, then the config-4 train step (tools/bench_prior.py --only train)
+  # alternating the in-tree library and each build (ROUNDS, default 3)
+  for v in "$@"; do
+    VQA_LIB_PATH=$v timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread \
+      tests/test_gpu_prior.py > $OUT/t_$(basename $v).log 2>&1 || { tail -40 $OUT/t_$(basename $v).log; exit 1; }
+    echo "tests $v: $(tail -1 $OUT/t_$(basename $v).log)"
+  done
+  for r in $(seq ${ROUNDS:-3}); do
+    for v in vae-based-music--deep-generative-models_amd/libvqa.so "$@"; do
+      echo "$(basename $v) $(VQA_LIB_PATH=$v timeout -k 10 300 python tools/bench_prior.py --only train --no-cpu 2>/dev/null | tail -1)"
+    done
+  done ;;
 suite)
   timeout -k 10 2400 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/suite.log 2>&1 \
     || { tail -60 $OUT/suite.log; exit 1; }

@@ -262,6 +262,11 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
   if constexpr (LNF)
     if (a.lng)
       for (int e = threadIdx.x; e < 2 * K; e += 64 * WAVES) Lg[e] = e < K ? a.lng[e] : a.lnb[e - K];
+  // the bias, staged once (after the LayerNorm parameters' slots): the epilogue reads it from LDS (a global load
+  // per output block, each used at once, was waited for in turn: NT round trips per tile)
+  float* Lb = Lg + 2 * K;
+  if (a.b)
+    for (int e = threadIdx.x; e < a.N; e += 64 * WAVES) Lb[e] = a.b[e];
   constexpr int CPR = K / VEC;
   for (int e = threadIdx.x; e < TAPS * a.N * CPR; e += 64 * WAVES) {
     const int n = e / CPR, q = e % CPR;
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
           if (nt * 16 >= a.N) break;
           const int c = nt * 16 + g4;
           f32x4 v = acc[nt];
-          if (a.b) v = v + f32x4{a.b[c], a.b[c + 1], a.b[c + 2], a.b[c + 3]};
+          if (a.b) v = v + *(const f32x4*)(Lb + c);
           if (a.r) v = v + r4[slot][nt].f();
           T* yp = (T*)a.y + row * a.ldy + c;
           if (a.accumulate) v = v + ld4((const T*)yp);
@@ -373,10 +378,7 @@ __global__ __launch_bounds__(64 * WAVES) void seqlin_d_kernel(SeqLinArgs a, int 
       for (int g = 0; g < NG; ++g) v[g] = *(const f32x4*)(E + row * ES + q * VEC + 4 * g);
       if (a.b)
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const float* bp = a.b + q * VEC + 4 * g;  // parameter views need not be 16-byte aligned
-          v[g] = v[g] + f32x4{bp[0], bp[1], bp[2], bp[3]};
-        }
+        for (int g = 0; g < NG; ++g) v[g] = v[g] + *(const f32x4*)(Lb + q * VEC + 4 * g);
       if (a.r) {
         chunk_widen<T>(rr[slot][i], u);
 #pragma unroll
@@ -1817,7 +1819,7 @@ static int launch_seqlin(const SeqLinArgs& a, hipStream_t s) {
     const int KS = a.K + 16 / (int)sizeof(T);
     const size_t lds = (size_t)a.taps * a.N * KS * sizeof(T) +
                        (a.taps == 1 ? (size_t)waves * 16 * (a.N + kSdEpad) * sizeof(float) : 0) +
-                       (a.lng ? (size_t)2 * a.K * sizeof(float) : 0);
+                       (size_t)(2 * a.K + a.N) * sizeof(float);  // LayerNorm slots (used or not) + the bias
     const void* fn = nullptr;
 #define VQA_SD(KK, TT)                                                                                         \
     if (a.K == KK && a.taps == TT)                                                                           \
