@@ -1228,23 +1228,23 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
     m[s] = -INFINITY; l[s] = 0.f; bv[s] = -INFINITY; bi[s] = 0; tl[s] = -INFINITY;
   }
   constexpr float L2E = 1.4426950408889634f;
+  // the tile's bias (slots past V: -inf) through LDS, loaded one tile ahead by wave 0 with the weight rows (read
+  // straight from global memory after the barrier, each tile waited for its bias loads there)
+  __shared__ __attribute__((aligned(16))) float Bt[64];
+  float bn = threadIdx.x < 64 && (int)threadIdx.x < a.V ? a.bias[threadIdx.x] : -INFINITY;
   for (int v0 = 0; v0 < a.V; v0 += 64) {
     __syncthreads();
     wn.store(W);
-    if (v0 + 64 < a.V) wn.load((const T*)a.wt, v0 + 64, a.V);
+    if (threadIdx.x < 64) Bt[threadIdx.x] = bn;
+    if (v0 + 64 < a.V) {
+      wn.load((const T*)a.wt, v0 + 64, a.V);
+      if (threadIdx.x < 64) bn = v0 + 64 + (int)threadIdx.x < a.V ? a.bias[v0 + 64 + threadIdx.x] : -INFINITY;
+    }
+    __syncthreads();
     // this lane's 16 vocab slots of the tile: v0 + 16 st + 4 g + i (slots past V: -inf)
     f32x4 bq[4];
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int vb = v0 + st * 16 + 4 * g;
-      if (vb + 4 <= a.V) {
-        bq[st] = *(const f32x4*)(a.bias + vb);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bq[st][i] = vb + i < a.V ? a.bias[vb + i] : -INFINITY;
-      }
-    }
-    __syncthreads();
+    for (int st = 0; st < 4; ++st) bq[st] = *(const f32x4*)(Bt + st * 16 + 4 * g);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float x[16];
@@ -1349,10 +1349,17 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
   float nl[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) nl[s] = -(lse[s] * L2E - __log2f(a.inv_count));
+  // the tile's bias through LDS, loaded one tile ahead (as head_fwd_kernel)
+  __shared__ __attribute__((aligned(16))) float Bt[64];
+  float bn = threadIdx.x < 64 && (int)threadIdx.x < a.V ? a.bias[threadIdx.x] : -INFINITY;
   for (int v0 = 0; v0 < a.V; v0 += 64) {
     __syncthreads();
     wn.store(W);
-    if (v0 + 64 < a.V) wn.load((const T*)a.wt, v0 + 64, a.V);
+    if (threadIdx.x < 64) Bt[threadIdx.x] = bn;
+    if (v0 + 64 < a.V) {
+      wn.load((const T*)a.wt, v0 + 64, a.V);
+      if (threadIdx.x < 64) bn = v0 + 64 + (int)threadIdx.x < a.V ? a.bias[v0 + 64 + threadIdx.x] : -INFINITY;
+    }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1360,14 +1367,7 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const f32x4 z = head_tile_x<T>(W + st * 16 * S, xf[s], S);
-        const int vb = v0 + st * 16 + 4 * g;
-        f32x4 bq;  // slots past V: -inf (probability 0)
-        if (vb + 4 <= a.V) {
-          bq = *(const f32x4*)(a.bias + vb);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) bq[i] = vb + i < a.V ? a.bias[vb + i] : -INFINITY;
-        }
+        const f32x4 bq = *(const f32x4*)(Bt + st * 16 + 4 * g);  // slots past V: -inf (probability 0)
 #pragma unroll
         for (int i = 0; i < 4; ++i) dl[st][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(z[i] + bq[i], L2E, nl[s]));
       }
@@ -1378,6 +1378,7 @@ __global__ __launch_bounds__(256) void head_bwd_dx_kernel(HeadArgs a) {
 #pragma unroll
         for (int kt = 0; kt < HK / 16; ++kt) acc[s][kt] = A::mm_rows(W + kt * 16, S, 32 * cc, p8, acc[s][kt]);
       }
+      __builtin_amdgcn_sched_barrier(0);  // one row subtile at a time (register pressure)
     }
   }
 #pragma unroll
