@@ -690,6 +690,15 @@ template <class T, int O, int PVX, int NEP, bool FW> constexpr int conv32_waves(
 // x-row byte offset that stays out of range after adding any tile base (|base| < 2^30)
 constexpr int kOOB = -0x40000000;
 
+// bf16 output tiles (no fused weight gradient) are staged through LDS over the x rows before they are stored: each
+// lane then writes whole 16-byte chunks of contiguous output rows (1 KB per wave store) instead of 8-byte pieces of
+// 16 rows (a quarter of a cache line each); the x region is sized for the staged tile (row pitch O + 8)
+template <class T, bool FW> constexpr bool conv32_staged() { return !FW && sizeof(T) == 2; }
+template <class T, int O, int PVX, bool FW> constexpr int conv32_xelems() {
+  constexpr int XS = 32 + 16 / (int)sizeof(T), XROWS = 256 / (32 / (16 / (int)sizeof(T))) * PVX;
+  return conv32_staged<T, FW>() && 128 * (O + 8) > XROWS * XS ? 128 * (O + 8) : XROWS * XS;
+}
+
 // O = 64: a 32 -> 64 conv, or the PAIR layout (conv-transpose forward, stride-2 data-gradient) whose
 // output row j holds the two full-resolution rows 2j, 2j+1 (32 channels each) — the bytes of (B, 2T, 32).
 template <class T, int O, int PVX, int NEP, bool FW>
@@ -708,7 +717,9 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* wl = (T*)smem;
   T* xl = wl + (size_t)a.K * O * WS;
-  char* el = (char*)(xl + (size_t)XROWS * XS);
+  char* el = (char*)(xl + (size_t)conv32_xelems<T, O, PVX, FW>());
+  constexpr bool SE = conv32_staged<T, FW>();
+  constexpr int OP = O + 8;  // staged row pitch (elements)
 
   const int tbeg = blockIdx.x * tpw, tend = min(ntiles, tbeg + tpw);
   if (tbeg >= tend) return;
@@ -811,6 +822,8 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
     }
     const __amdgpu_buffer_rsrc_t ry = item_rsrc(a.y, (long long)n * obytes, obytes);
     const int yb = t0 * O * ESZ;
+    T* stg = xl + (size_t)wave * RW * OP;  // SE: this wave's staged rows
+    if constexpr (SE) __syncthreads();     // every wave's MFMA reads of the x rows are done
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int tl = wave * RW + nt * 16 + (lane & 15);
@@ -825,7 +838,26 @@ void conv32_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
           for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
         }
         if (do_res) v = ld4(rl + eidx) + v;
-        store_out4<T>(ry, eidx * ESZ + yb, v);
+        if constexpr (SE) {
+          const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *(bf16x4*)(stg + (nt * 16 + (lane & 15)) * OP + o) = ob;
+        } else {
+          store_out4<T>(ry, eidx * ESZ + yb, v);
+        }
+      }
+    }
+    if constexpr (SE) {
+      // the wave's RW rows are contiguous in the output: 16-byte chunks, rows past the item dropped by the range
+      // check (a chunk never straddles a PAIR half: 32 channels = 4 chunks)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int CPRO = O * 2 / 16, NCH = RW * CPRO / 64;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int e = lane + 64 * i, r = e / CPRO, q = e - r * CPRO;
+        const u32x4 c = *(const u32x4*)(stg + r * OP + q * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(c, ry, ((wave * RW + r) * O + q * 8) * 2 + yb, 0, 0);
       }
     }
     if constexpr (FW) {
@@ -1501,8 +1533,8 @@ static int launch_gather_mfma(const GatherArgs& a, hipStream_t s) {
 // ---- the 32-channel kernel
 template <class T, int O, int PVX, int NEP, bool FW>
 static int launch_conv32_k(const GatherArgs& a, hipStream_t s, int* nwg_out) {
-  constexpr int ESZ = (int)sizeof(T), XS = 32 + lds_pad<T>(), XROWS = 256 / (32 / (16 / ESZ)) * PVX;
-  const size_t lds = ((size_t)a.K * O * XS + (size_t)XROWS * XS) * ESZ + (size_t)NEP * 128 * O * ESZ;
+  constexpr int ESZ = (int)sizeof(T), XS = 32 + lds_pad<T>();
+  const size_t lds = ((size_t)a.K * O * XS + (size_t)conv32_xelems<T, O, PVX, FW>()) * ESZ + (size_t)NEP * 128 * O * ESZ;
   const void* fn = (const void*)conv32_kernel<T, O, PVX, NEP, FW>;
   static size_t lds_set = 0;
   const int rc = ensure_dyn_lds(fn, lds, &lds_set, "conv32_kernel");
