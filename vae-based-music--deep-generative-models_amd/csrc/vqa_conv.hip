@@ -475,6 +475,19 @@ struct TileRegs {
   }
 };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t item_rsrc(const void* base, long long off, unsigned bytes) {
+  const unsigned long long p = (unsigned long long)base + (unsigned long long)off;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+  void* q = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+
 // MFMA gather conv, persistent and software-pipelined. Each workgroup (4 waves) owns a contiguous range
 // of TM-row tiles of one or more items (a tile's halo rows were just read by its predecessor on the
 // same CU), stages the weights once, and keeps TWO tiles in flight in registers (tiles i+1, i+2) while
@@ -547,6 +560,14 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
   A.store(S0, xl, XS, (char*)ml, (char*)rl, relu);
   __syncthreads();
 
+  // bf16 tiles without epilogue operands: the output rows staged in the (then unused) epilogue-operand region and
+  // stored as contiguous 16-byte chunks (the 8-byte per-lane stores wrote a quarter of a cache line each)
+  constexpr int OP = O + 8;
+  const int rvalid_ = pair ? a.T_full : a.T_out;
+  const bool se = sizeof(T) == 2 && !do_mask && !do_res && (long long)rvalid_ * erow * ESZ < (1ll << 31);
+  T* stg = ml + (size_t)wave * RW * OP;
+  static_assert(TM * (O + 8) <= 2 * TM * O, "staged tile fits the two epilogue-operand tiles");
+
   // one tile: MFMAs out of LDS, epilogue operands out of LDS, stores to global
   auto run_tile = [&](int tile) {
     const int n = tile / ntm, t0 = (tile - n * ntm) * TM;
@@ -573,6 +594,37 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
           for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = M::mma(af[mt], bf, acc[mt][nt]);
         }
       }
+    }
+    if (se) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int o = mt * 16 + 4 * (lane >> 4);
+          f32x4 v = acc[mt][nt];
+          if (a.bias) {
+            const f32x4 bp = *(const f32x4*)(bias_l + o);
+            v = f32x4{v[0] + bp[0], v[1] + bp[1], v[2] + bp[2], v[3] + bp[3]};
+          }
+          const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *(bf16x4*)(stg + (nt * 16 + (lane & 15)) * OP + o) = ob;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the wave's RW output rows are contiguous (PAIR: row t holds full-resolution rows 2t, 2t+1); rows past the
+      // item are dropped by the range check (a 16-byte chunk never straddles a PAIR half)
+      const unsigned ib = (unsigned)((long long)rvalid_ * erow * ESZ);
+      const __amdgpu_buffer_rsrc_t ry = item_rsrc(a.y, (long long)n * ib, ib);
+      constexpr int CPRO = O * 2 / 16, NCH = RW * CPRO / 64;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int e = lane + 64 * i, r = e / CPRO, q = e - r * CPRO;
+        const u32x4 c = *(const u32x4*)(stg + r * OP + q * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(c, ry, ((t0 + wave * RW + r) * O + q * 8) * 2, 0, 0);
+      }
+      return;
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -647,18 +699,6 @@ void gather_mfma_kernel(GatherArgs a, int ntm, int ntiles, int tpw) {
 //  * the tile is held in registers two tiles ahead (T14) exactly as in gather_mfma_kernel.
 // FW additionally accumulates the weight gradient of a stride-1 data-gradient from the staged tiles
 // (vqa_conv1d_bwd_data_weight): epilogue tensor 0 is then the conv input u.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t item_rsrc(const void* base, long long off, unsigned bytes) {
-  const unsigned long long p = (unsigned long long)base + (unsigned long long)off;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
-  void* q = (void*)(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
 template <class T> __device__ __forceinline__ u32x4 relu_chunk(u32x4 v);
 __device__ __forceinline__ unsigned relu_pk_bf16(unsigned w) {
   const s16x2 z = {0, 0};
